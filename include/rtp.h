@@ -1,0 +1,151 @@
+/*
+ * rtp.h -- C ABI of the MI355X-native Monte Carlo path tracer (librtp.so).
+ *
+ * Drop-in boundary for vtkm::rendering::MapperPathTracer
+ * (reference MapperPathTracer.h:44-159, MapperPathTracer.cxx:94-406).  Plain
+ * pointers and sizes only; no VTK-m, HIP or torch types in the signatures.
+ * The reference exposes a C++ class, so the "binding" a maintainer adds is
+ * the header-only C++ shim include/rtp/mapper.hpp (same class and method
+ * names) -- see INTEGRATION.md.
+ *
+ * Mapping to the reference:
+ *   rtp_create / rtp_destroy      MapperPathTracer ctor/dtor (:94-153); one
+ *                                 context per GPU (HIP device ordinal).
+ *   rtp_set_scene                 the scene half of the ctor (matIdx, texIdx,
+ *                                 matType, texType, tex) + the cell set and
+ *                                 coordinates handed to RenderCells
+ *                                 (extract/buildBVH, :178-197, :437-449) +
+ *                                 the hard-coded light coupling (:141-148,
+ *                                 :218, :467).
+ *   rtp_render                    SetCanvas + RenderCells (:155-172,
+ *                                 :356-383): fills the canvas colour buffer
+ *                                 (Vec4f per pixel) with the UN-normalised
+ *                                 per-pixel sum over spp samples.
+ *   rtp_render_device             same, output already in device memory (the
+ *                                 HBM-resident path used by bench.py and the
+ *                                 multi-GPU tile shard).
+ *   rtp_normalize                 NormalizeFunctor, main.cc:253-287.
+ *   rtp_write_pnm                 save(), main.cc:325-384 (P3, buffer order).
+ *   rtp_cornell_box               CornellBox::buildDataSet (CornellBox.cpp).
+ *
+ * Errors: every entry point returns an rtp_status; rtp_last_error() gives a
+ * thread-local message (the reference throws vtkm::cont::ErrorBadValue).
+ */
+#ifndef RTP_H
+#define RTP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTP_ABI_VERSION 1
+
+typedef enum {
+  RTP_OK = 0,
+  RTP_ERR_INVALID_ARGUMENT = -1, /* ErrorBadValue in the reference */
+  RTP_ERR_NO_SCENE = -2,
+  RTP_ERR_DEVICE = -3,           /* HIP runtime failure / no GPU */
+  RTP_ERR_OUT_OF_MEMORY = -4,
+} rtp_status;
+
+typedef struct rtp_context rtp_context;
+
+/* vtkm::rendering::Camera fields read by pathtracing::Camera::SetParameters
+ * (Camera.cxx:624-637).  Zoom and clipping range do not affect the path. */
+typedef struct {
+  float position[3];
+  float look_at[3];
+  float view_up[3];
+  float fov_y_deg; /* applied to both axes (Camera.cxx:925-931) */
+} rtp_camera;
+
+/* Scene in the reference's representation.  quad_points holds, per quad,
+ * the QuadExtractor point ids [p0 p1 p2 p3] (= QuadIds[1..4]); the Lagae-
+ * Dutre test takes v00=p0, v10=p1, v11=p2, v01=p3 (Surface.h:174). */
+typedef struct {
+  const float* points; /* float3[n_points] */
+  int32_t n_points;
+  const int32_t* quad_points; /* int32[4*n_quads] */
+  const int32_t* quad_mat;    /* matIdx[0] */
+  const int32_t* quad_tex;    /* texIdx[0] */
+  int32_t n_quads;
+  const int32_t* sphere_point;  /* SphereIds */
+  const float* sphere_radius;   /* SphereRadii */
+  const int32_t* sphere_mat;    /* matIdx[1] */
+  const int32_t* sphere_tex;    /* texIdx[1] */
+  int32_t n_spheres;
+  const int32_t* mat_type; /* 0 lambertian, 1 diffuse light, 2 dielectric */
+  int32_t n_mat;
+  const int32_t* tex_type;
+  int32_t n_tex_type;
+  const float* tex_rgb; /* float3[n_tex] */
+  int32_t n_tex;
+  int32_t light_quad_points[4]; /* light_box_pointids[1..4] (8,9,10,11) */
+  int32_t light_sphere_point;   /* light_sphere_pointids[0] (48); radius = sphere_radius[0] */
+  float ior;                    /* DielectricWorklet ref_idx (1.5) */
+} rtp_scene_desc;
+
+typedef struct {
+  uint64_t samples;      /* pixels * spp */
+  uint64_t live_bounces; /* ray-bounces processed while the path was alive */
+  uint64_t nan_pixels;   /* pixels whose rgb sum is NaN before normalisation */
+  double kernel_ms;      /* device time of the render kernel(s) */
+} rtp_stats;
+
+/* optional per-pixel diagnostics (device or host pointers matching the call) */
+typedef struct {
+  uint32_t* final_seed;   /* RNG state after the last sample (nullable) */
+  uint32_t* live_bounces; /* live ray-bounces per pixel (nullable) */
+} rtp_pixel_aux;
+
+const char* rtp_last_error(void);
+int32_t rtp_abi_version(void);
+
+rtp_status rtp_create(int32_t device, rtp_context** out);
+void rtp_destroy(rtp_context* ctx);
+
+rtp_status rtp_set_scene(rtp_context* ctx, const rtp_scene_desc* scene);
+
+/* Full canvas render into host memory (rgba_out: float4[nx*ny]). */
+rtp_status rtp_render(rtp_context* ctx, const rtp_camera* cam, int32_t nx, int32_t ny, int32_t spp,
+                      int32_t depth, uint32_t seed_base, float* rgba_out, rtp_stats* stats);
+
+/* Device-resident render of a pixel set on hip_stream (0 = null stream).
+ * Pixels: d_pixel_ids (device int64[pixel_count]) when non-NULL, else the
+ * contiguous range [pixel_begin, pixel_begin+pixel_count).  d_rgba_out is a
+ * device float4[pixel_count] (entry k <-> k-th pixel of the set).  aux
+ * pointers, when non-NULL, are device arrays of pixel_count.  Asynchronous:
+ * returns after enqueueing; stats->kernel_ms is only filled when
+ * stats != NULL, which synchronises the stream. */
+rtp_status rtp_render_device(rtp_context* ctx, const rtp_camera* cam, int32_t nx, int32_t ny, int32_t spp,
+                             int32_t depth, uint32_t seed_base, int64_t pixel_begin, int64_t pixel_count,
+                             const int64_t* d_pixel_ids, float* d_rgba_out, const rtp_pixel_aux* aux,
+                             void* hip_stream, rtp_stats* stats);
+
+/* Host-memory variant of rtp_render_device for an arbitrary pixel list
+ * (golden pixel subsets); aux pointers are host arrays. */
+rtp_status rtp_render_pixels(rtp_context* ctx, const rtp_camera* cam, int32_t nx, int32_t ny, int32_t spp,
+                             int32_t depth, uint32_t seed_base, const int64_t* pixel_ids, int64_t pixel_count,
+                             float* rgba_out, const rtp_pixel_aux* aux, rtp_stats* stats);
+
+/* Host-side helpers of the application layer (main.cc). */
+rtp_status rtp_normalize(float* rgba, int64_t n_pixels, int32_t spp);
+rtp_status rtp_write_pnm(const char* path, const float* rgba, int32_t nx, int32_t ny);
+
+/* CornellBox::buildDataSet.  variant 0: the reference scene; variant 1:
+ * sphere moved to (190,90,190) so the dielectric is visible.  The returned
+ * descriptor points into library-owned static storage. */
+rtp_status rtp_cornell_box(int32_t variant, rtp_scene_desc* out);
+
+/* Diagnostics: evaluate a device primitive elementwise (tests only).
+ * kind 0: glibc-exact sinf port, 1: cosf port, 2: 1/sqrtf(x) (RMagnitude),
+ * 3: wang32 (bit pattern in/out), 4: which(hash) thresholds. */
+rtp_status rtp_eval_primitive(rtp_context* ctx, int32_t kind, const void* in, void* out, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTP_H */

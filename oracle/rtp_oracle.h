@@ -1,0 +1,100 @@
+/*
+ * rtp_oracle.h -- CPU restatement of m-kim/raytracingtherestofyourlife's
+ * Monte Carlo path-tracing loop (MapperPathTracer::RenderCellsImpl).
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (librtp.so, the HIP
+ * kernels, the Python package) links, loads or calls this code.  It is used
+ * by tests/ (as the parity checker), by __graft_entry__.smoke() (checker) and
+ * by bench.py's cpu_baseline leg (timed CPU baseline, kind "port").
+ *
+ * Parity status: the reference cannot be compiled here (needs VTK-m, absent,
+ * see SURVEY.md 8c), so this restatement is pinned by (i) known-answer tests
+ * probed on this host (RNG, glibc sinf/cosf bit-exactness, g++ argument
+ * evaluation order) and (ii) the two internal variants (scalar per-pixel and
+ * stage-structured SoA) agreeing bit-for-bit.  VTK-m behaviour that the
+ * reference relies on is restated from its published semantics and each
+ * assumption is listed in DESIGN.md section "Oracle assumptions".
+ */
+#ifndef RTP_ORACLE_H
+#define RTP_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTPO_MAX_POINTS 8192
+#define RTPO_MAX_QUADS 2048
+#define RTPO_MAX_SPHERES 2048
+#define RTPO_MAX_MATS 16
+
+/* Scene in the reference's own representation (CornellBox.cpp:141-418,
+ * MapperPathTracer.cxx:141-148, 178-197).  quad_ids rows are the
+ * QuadExtractor layout [cellId, p0, p1, p2, p3]. */
+typedef struct {
+  int32_t n_points;
+  float points[RTPO_MAX_POINTS][3];
+  int32_t n_quads;
+  int32_t quad_ids[RTPO_MAX_QUADS][5];
+  int32_t quad_mat[RTPO_MAX_QUADS]; /* matIdx[0] */
+  int32_t quad_tex[RTPO_MAX_QUADS]; /* texIdx[0] */
+  int32_t n_spheres;
+  int32_t sphere_point[RTPO_MAX_SPHERES]; /* SphereIds */
+  float sphere_radius[RTPO_MAX_SPHERES];  /* SphereRadii */
+  int32_t sphere_mat[RTPO_MAX_SPHERES];   /* matIdx[1] */
+  int32_t sphere_tex[RTPO_MAX_SPHERES];   /* texIdx[1] */
+  int32_t n_mat;
+  int32_t mat_type[RTPO_MAX_MATS];
+  int32_t n_tex_type;
+  int32_t tex_type[RTPO_MAX_MATS];
+  int32_t n_tex;
+  float tex[RTPO_MAX_MATS][3];
+  int32_t light_box_pointids[5]; /* (0,8,9,10,11) MapperPathTracer.cxx:141 */
+  int32_t light_sphere_point;    /* 48, MapperPathTracer.cxx:145 */
+  float ior;                     /* 1.5, MapperPathTracer.cxx:467 */
+} rtpo_scene;
+
+/* Camera constants shared by every RayGen invocation:
+ * cam[0..2] eye, [3..5] nlook, [6..8] delta_x, [9..11] delta_y. */
+void rtpo_camera_setup(const float pos[3], const float look_at[3], const float up[3], float fov_y_deg,
+                       int32_t nx, int32_t ny, float cam[12]);
+
+/* variant 0: reference scene (CornellBox.cpp:141-418, glass sphere at x=-335,
+ *            outside the box).
+ * variant 1: same, sphere moved to (190,90,190) (notebook cell 2) so the
+ *            dielectric path is exercised. */
+void rtpo_cornell_box(int32_t variant, rtpo_scene* out);
+
+/* Scalar per-pixel render of an arbitrary pixel subset (pixels are fully
+ * independent because seed[i] = seed_base + i, MapperPathTracer.cxx:265-267).
+ * out_rgba[4*k..] receives the un-normalised canvas sum for pixels[k]
+ * (alpha := 0); out_seed / out_live (nullable) the final RNG state and the
+ * number of live ray-bounces of that pixel.  nthreads <= 0: all cores. */
+void rtpo_render_pixels(const rtpo_scene* sc, const float cam[12], int32_t nx, int32_t ny, int32_t spp,
+                        int32_t depth, uint32_t seed_base, const int64_t* pixels, int64_t npix,
+                        float* out_rgba, uint32_t* out_seed, uint32_t* out_live, int32_t nthreads);
+
+/* Stage-structured SoA render of the full nx*ny canvas: the same per-stage
+ * passes over all rays as RenderCellsImpl (no compaction, cost ~ N*S*D).
+ * This is the timed CPU baseline.  Must agree bit-for-bit with
+ * rtpo_render_pixels.  rows restricts work to image rows [row_begin,row_end)
+ * (a bounded sample for timing); pass 0, ny for the whole image. */
+int32_t rtpo_render_soa(const rtpo_scene* sc, const float cam[12], int32_t nx, int32_t ny, int32_t spp,
+                        int32_t depth, uint32_t seed_base, int32_t row_begin, int32_t row_end,
+                        float* out_rgba, uint32_t* out_seed, uint32_t* out_live, int32_t nthreads);
+
+/* NormalizeFunctor (main.cc:253-287): de-NaN rgb, then sqrt(x / spp). */
+void rtpo_normalize(float* rgba, int64_t n, int32_t spp);
+
+/* primitives, exported for known-answer tests */
+uint32_t rtpo_wang32(uint32_t seed);
+float rtpo_randf(uint32_t* seed);
+float rtpo_sinf(float x);
+float rtpo_cosf(float x);
+int32_t rtpo_which(uint32_t hash_value);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

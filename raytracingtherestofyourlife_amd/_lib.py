@@ -1,0 +1,110 @@
+"""ctypes binding of librtp.so (include/rtp.h).
+
+There is no CPU fallback: if the HIP library is missing or fails to load,
+every entry point raises.  The product path is the HIP path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librtp.so")
+
+RTP_OK = 0
+RTP_ERR_INVALID_ARGUMENT = -1
+RTP_ERR_NO_SCENE = -2
+RTP_ERR_DEVICE = -3
+RTP_ERR_OUT_OF_MEMORY = -4
+
+f32p = ctypes.POINTER(ctypes.c_float)
+i32p = ctypes.POINTER(ctypes.c_int32)
+u32p = ctypes.POINTER(ctypes.c_uint32)
+i64p = ctypes.POINTER(ctypes.c_int64)
+
+
+class RtpCamera(ctypes.Structure):
+    _fields_ = [("position", ctypes.c_float * 3), ("look_at", ctypes.c_float * 3),
+                ("view_up", ctypes.c_float * 3), ("fov_y_deg", ctypes.c_float)]
+
+
+class RtpSceneDesc(ctypes.Structure):
+    _fields_ = [
+        ("points", f32p), ("n_points", ctypes.c_int32),
+        ("quad_points", i32p), ("quad_mat", i32p), ("quad_tex", i32p), ("n_quads", ctypes.c_int32),
+        ("sphere_point", i32p), ("sphere_radius", f32p), ("sphere_mat", i32p), ("sphere_tex", i32p),
+        ("n_spheres", ctypes.c_int32),
+        ("mat_type", i32p), ("n_mat", ctypes.c_int32),
+        ("tex_type", i32p), ("n_tex_type", ctypes.c_int32),
+        ("tex_rgb", f32p), ("n_tex", ctypes.c_int32),
+        ("light_quad_points", ctypes.c_int32 * 4), ("light_sphere_point", ctypes.c_int32),
+        ("ior", ctypes.c_float),
+    ]
+
+
+class RtpStats(ctypes.Structure):
+    _fields_ = [("samples", ctypes.c_uint64), ("live_bounces", ctypes.c_uint64),
+                ("nan_pixels", ctypes.c_uint64), ("kernel_ms", ctypes.c_double)]
+
+
+class RtpPixelAux(ctypes.Structure):
+    _fields_ = [("final_seed", u32p), ("live_bounces", u32p)]
+
+
+EXPORTED_SYMBOLS = [
+    "rtp_last_error", "rtp_abi_version", "rtp_create", "rtp_destroy", "rtp_set_scene", "rtp_render",
+    "rtp_render_device", "rtp_render_pixels", "rtp_normalize", "rtp_write_pnm", "rtp_cornell_box",
+    "rtp_eval_primitive",
+]
+
+
+class RtpError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"rtp error {status}: {msg}")
+        self.status = status
+
+
+_lib = None
+
+
+def load(build_if_missing: bool = True) -> ctypes.CDLL:
+    """Load librtp.so (building it with hipcc first if it is absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        if not build_if_missing:
+            raise RuntimeError(f"{LIB_PATH} is missing; run raytracingtherestofyourlife_amd/build.py")
+        from . import build as _build
+        _build.build()
+    L = ctypes.CDLL(LIB_PATH)
+    L.rtp_last_error.restype = ctypes.c_char_p
+    L.rtp_abi_version.restype = ctypes.c_int32
+    vp = ctypes.c_void_p
+    L.rtp_create.argtypes = [ctypes.c_int32, ctypes.POINTER(vp)]
+    L.rtp_destroy.argtypes = [vp]
+    L.rtp_destroy.restype = None
+    L.rtp_set_scene.argtypes = [vp, ctypes.POINTER(RtpSceneDesc)]
+    L.rtp_render.argtypes = [vp, ctypes.POINTER(RtpCamera), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                             ctypes.c_int32, ctypes.c_uint32, f32p, ctypes.POINTER(RtpStats)]
+    L.rtp_render_device.argtypes = [vp, ctypes.POINTER(RtpCamera), ctypes.c_int32, ctypes.c_int32,
+                                    ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_int64,
+                                    ctypes.c_int64, vp, vp, ctypes.POINTER(RtpPixelAux), vp,
+                                    ctypes.POINTER(RtpStats)]
+    L.rtp_render_pixels.argtypes = [vp, ctypes.POINTER(RtpCamera), ctypes.c_int32, ctypes.c_int32,
+                                    ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, i64p, ctypes.c_int64, f32p,
+                                    ctypes.POINTER(RtpPixelAux), ctypes.POINTER(RtpStats)]
+    L.rtp_normalize.argtypes = [f32p, ctypes.c_int64, ctypes.c_int32]
+    L.rtp_write_pnm.argtypes = [ctypes.c_char_p, f32p, ctypes.c_int32, ctypes.c_int32]
+    L.rtp_cornell_box.argtypes = [ctypes.c_int32, ctypes.POINTER(RtpSceneDesc)]
+    L.rtp_eval_primitive.argtypes = [vp, ctypes.c_int32, vp, vp, ctypes.c_int64]
+    for name in EXPORTED_SYMBOLS:
+        if name not in ("rtp_last_error", "rtp_abi_version", "rtp_destroy"):
+            getattr(L, name).restype = ctypes.c_int32
+    _lib = L
+    return L
+
+
+def check(status: int) -> None:
+    if status != RTP_OK:
+        raise RtpError(status, load().rtp_last_error().decode(errors="replace"))

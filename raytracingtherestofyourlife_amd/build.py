@@ -1,0 +1,58 @@
+"""Build librtp.so (HIP kernels + C ABI) in-tree for gfx950 with hipcc.
+
+The shared object lands next to this file so it travels to the GPU box with
+the repository snapshot.  Flags that the parity contract depends on:
+  -ffp-contract=off      no a*b+c -> fma contraction (the reference's x86-64
+                         g++ build has no FMA);
+  no -ffast-math, HIP's default correctly-rounded f32 div/sqrt, denormals kept.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "librtp.so")
+SOURCES = ["rtp_kernels.hip", "rtp_host.cpp", "scene_cornell.cpp"]
+HEADERS = ["rtp_device.hpp", "rtp_layout.hpp", os.path.join("..", "..", "include", "rtp.h")]
+ARCH = os.environ.get("RTP_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: librtp.so cannot be built")
+
+
+def flags() -> list[str]:
+    return ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+            "-fno-fast-math", "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+
+
+def stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.abspath(__file__)]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not stale():
+        return LIB
+    cmd = [hipcc(), *flags(), "-o", LIB + ".tmp", *[os.path.join(CSRC, s) for s in SOURCES]]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stdout}\n{res.stderr}")
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,474 @@
+// rtp_host.cpp -- host side of librtp.so: the C ABI declared in include/rtp.h.
+//
+// Mirrors vtkm::rendering::MapperPathTracer (MapperPathTracer.cxx:94-538):
+// the scene/material tables, the camera set-up of pathtracing::Camera
+// (Camera.cxx:437-474, 624-776, 879-960) and the render entry point.  All
+// ray-independent quantities are precomputed here with the reference's own
+// float operations (compiled with -ffp-contract=off; x86-64 SSE2 arithmetic
+// is IEEE single/double, the same as the reference's g++ build).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rtp.h"
+#include "rtp_layout.hpp"
+
+extern "C" hipError_t rtp_launch_render(const rtp::KParams* p, hipStream_t stream);
+extern "C" hipError_t rtp_launch_eval_primitive(int kind, const void* in, void* out, int64_t n, hipStream_t stream);
+
+namespace {
+
+thread_local std::string g_err;
+
+rtp_status fail(rtp_status st, const std::string& msg) {
+  g_err = msg;
+  return st;
+}
+rtp_status hip_fail(hipError_t e, const char* what) {
+  return fail(e == hipErrorOutOfMemory ? RTP_ERR_OUT_OF_MEMORY : RTP_ERR_DEVICE,
+              std::string(what) + ": " + hipGetErrorString(e));
+}
+#define HIP_TRY(expr)                                 \
+  do {                                                \
+    hipError_t e_ = (expr);                           \
+    if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+  } while (0)
+
+// ---------------------------------------------------- host vector math ---
+struct v3 {
+  float x, y, z;
+};
+inline v3 sub(v3 a, v3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline v3 scl(v3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+inline float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline v3 cross(v3 a, v3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+inline float rmag(v3 a) { return 1 / std::sqrt(dot(a, a)); }
+inline v3 normalize(v3 a) { return scl(a, rmag(a)); }  // vtkm::Normalize (CPU build)
+inline v3 ld(const float* p) { return {p[0], p[1], p[2]}; }
+inline void st(float* d, v3 a) { d[0] = a.x, d[1] = a.y, d[2] = a.z; }
+
+// which = min(3, int(r*3+1)), r = float(t)/4294967295.f  (PdfWorklet.h:20)
+int which_of_hash(uint32_t t) {
+  float r = (float)t / 4294967295.f;
+  int w = (int)(r * 3 + 1);
+  return w < 3 ? w : 3;
+}
+// smallest hash value with which >= w (which is monotone in t)
+uint32_t which_threshold(int w) {
+  uint64_t lo = 0, hi = 0x100000000ull;  // answer in [lo, hi]
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) / 2;
+    if (which_of_hash((uint32_t)mid) >= w)
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  return lo > 0xffffffffull ? 0xffffffffu : (uint32_t)lo;
+}
+
+void fill_quad(rtp::DevQuad& Q, v3 q, v3 r, v3 s, v3 t) {
+  std::memset(&Q, 0, sizeof(Q));
+  st(Q.v00, q);
+  st(Q.e01, sub(r, q));
+  st(Q.e03, sub(t, q));
+  st(Q.v11, s);
+  st(Q.e21, sub(r, s));
+  st(Q.e23, sub(t, s));
+  st(Q.n, normalize(cross(sub(r, q), sub(s, q))));  // TriangleNormal(q,r,s), Surface.h:182-183
+}
+
+bool bit_equal(const float* a, const float* b, int n) { return std::memcmp(a, b, sizeof(float) * n) == 0; }
+
+}  // namespace
+
+struct rtp_context {
+  int device = 0;
+  rtp::DevScene* d_scene = nullptr;
+  bool has_scene = false;
+  float* d_hist = nullptr;
+  size_t hist_bytes = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+extern "C" {
+
+const char* rtp_last_error(void) { return g_err.c_str(); }
+int32_t rtp_abi_version(void) { return RTP_ABI_VERSION; }
+
+rtp_status rtp_create(int32_t device, rtp_context** out) {
+  if (!out) return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_create: out is NULL");
+  *out = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0) return fail(RTP_ERR_DEVICE, "rtp_create: no HIP device available");
+  if (device < 0 || device >= n) return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_create: device ordinal out of range");
+  HIP_TRY(hipSetDevice(device));
+  rtp_context* c = new rtp_context();
+  c->device = device;
+  e = hipMalloc(&c->d_scene, sizeof(rtp::DevScene));
+  if (e != hipSuccess) {
+    delete c;
+    return hip_fail(e, "hipMalloc(scene)");
+  }
+  HIP_TRY(hipEventCreate(&c->ev0));
+  HIP_TRY(hipEventCreate(&c->ev1));
+  *out = c;
+  return RTP_OK;
+}
+
+void rtp_destroy(rtp_context* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->d_scene) hipFree(c->d_scene);
+  if (c->d_hist) hipFree(c->d_hist);
+  if (c->ev0) hipEventDestroy(c->ev0);
+  if (c->ev1) hipEventDestroy(c->ev1);
+  delete c;
+}
+
+// extract + buildBVH (MapperPathTracer.cxx:178-197, 437-449) and the light
+// coupling of the constructor (:141-148).  Quads that repeat an earlier quad
+// bit-for-bit (same vertices in the same order, same material and texture --
+// buildBox emits two such pairs per box, CornellBox.cpp:114-137) are dropped:
+// under the strict '<' closest test the later copy can never win, so the hit
+// record is unchanged.
+rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
+  if (!c || !s) return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_set_scene: NULL argument");
+  if (s->n_points <= 0 || !s->points) return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_set_scene: no points");
+  if (s->n_quads < 0 || s->n_spheres < 0 || s->n_spheres > rtp::kMaxSpheres)
+    return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_set_scene: bad primitive counts");
+  if (s->n_spheres < 1)
+    return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_set_scene: the light sphere radius is SphereRadii[0]; need >= 1 sphere");
+  auto pt_ok = [&](int32_t id) { return id >= 0 && id < s->n_points; };
+  auto mat_ok = [&](int32_t m) { return m >= 0 && m < s->n_mat && s->mat_type[m] >= 0 && s->mat_type[m] <= 2; };
+  auto tex_ok = [&](int32_t t) {
+    return t >= 0 && t < s->n_tex_type && s->tex_type[t] >= 0 && s->tex_type[t] < s->n_tex;
+  };
+  rtp::DevScene* h = new rtp::DevScene();
+  std::memset(h, 0, sizeof(*h));
+  std::vector<int> kept;
+  for (int q = 0; q < s->n_quads; q++) {
+    const int32_t* id = s->quad_points + 4 * q;
+    for (int k = 0; k < 4; k++)
+      if (!pt_ok(id[k])) {
+        delete h;
+        return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_set_scene: quad point id out of range");
+      }
+    if (!mat_ok(s->quad_mat[q]) || !tex_ok(s->quad_tex[q])) {
+      delete h;
+      return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_set_scene: quad material/texture index out of range");
+    }
+    bool dup = false;
+    for (int j : kept) {
+      const int32_t* jd = s->quad_points + 4 * j;
+      bool same = s->quad_mat[j] == s->quad_mat[q] && s->quad_tex[j] == s->quad_tex[q];
+      for (int k = 0; k < 4 && same; k++) same = bit_equal(s->points + 3 * jd[k], s->points + 3 * id[k], 3);
+      if (same) {
+        dup = true;
+        break;
+      }
+    }
+    if (dup) continue;
+    if ((int)kept.size() >= rtp::kMaxQuads) {
+      delete h;
+      return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_set_scene: too many distinct quads");
+    }
+    rtp::DevQuad& Q = h->quads[kept.size()];
+    fill_quad(Q, ld(s->points + 3 * id[0]), ld(s->points + 3 * id[1]), ld(s->points + 3 * id[2]),
+              ld(s->points + 3 * id[3]));
+    Q.mt = s->mat_type[s->quad_mat[q]];
+    st(Q.alb, ld(s->tex_rgb + 3 * s->tex_type[s->quad_tex[q]]));
+    kept.push_back(q);
+  }
+  h->n_quads = (int32_t)kept.size();
+  for (int k = 0; k < s->n_spheres; k++) {
+    if (!pt_ok(s->sphere_point[k]) || !mat_ok(s->sphere_mat[k]) || !tex_ok(s->sphere_tex[k])) {
+      delete h;
+      return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_set_scene: sphere index out of range");
+    }
+    rtp::DevSphere& S = h->spheres[k];
+    st(S.c, ld(s->points + 3 * s->sphere_point[k]));
+    S.r = s->sphere_radius[k];
+    S.rr = S.r * S.r;
+    S.mt = s->mat_type[s->sphere_mat[k]];
+    st(S.alb, ld(s->tex_rgb + 3 * s->tex_type[s->sphere_tex[k]]));
+  }
+  h->n_spheres = s->n_spheres;
+  // lights (MapperPathTracer.cxx:141-148): light quad = light_box_pointids[1..4]
+  const int32_t* lq = s->light_quad_points;
+  for (int k = 0; k < 4; k++)
+    if (!pt_ok(lq[k])) {
+      delete h;
+      return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_set_scene: light quad point id out of range");
+    }
+  if (!pt_ok(s->light_sphere_point)) {
+    delete h;
+    return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_set_scene: light sphere point id out of range");
+  }
+  v3 q = ld(s->points + 3 * lq[0]), r = ld(s->points + 3 * lq[1]), ss = ld(s->points + 3 * lq[2]),
+     t = ld(s->points + 3 * lq[3]);
+  fill_quad(h->light.quad, q, r, ss, t);
+  {
+    float qr = std::sqrt(dot(sub(r, q), sub(r, q)));  // vtkm::Magnitude
+    float qt = std::sqrt(dot(sub(t, q), sub(t, q)));
+    h->light.area = qr * qt;  // PdfWorklet.h:236-239
+  }
+  // QuadWorkletGenerateDir uses pts[pointIndex[1]] and pts[pointIndex[3]]
+  {
+    float x0 = q.x, x1 = ss.x, z0 = q.z, z1 = ss.z, y0 = q.y, y1 = q.y;
+    h->light.gx0 = x0, h->light.gdx = x1 - x0;
+    h->light.gy0 = y0, h->light.gdy = y1 - y0;
+    h->light.gz0 = z0, h->light.gdz = z1 - z0;
+  }
+  st(h->light.sc, ld(s->points + 3 * s->light_sphere_point));
+  h->light.sr = s->sphere_radius[0];
+  h->light.srr = h->light.sr * h->light.sr;
+  h->ior = s->ior;
+  h->which_t1 = which_threshold(2);
+  h->which_t2 = which_threshold(3);
+  hipError_t e = hipSetDevice(c->device);
+  if (e == hipSuccess) e = hipMemcpy(c->d_scene, h, sizeof(*h), hipMemcpyHostToDevice);
+  delete h;
+  if (e != hipSuccess) return hip_fail(e, "rtp_set_scene upload");
+  c->has_scene = true;
+  return RTP_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// pathtracing::Camera::SetParameters -> CreateRaysImpl -> RayGen ctor
+void camera_setup(const rtp_camera* cam, int32_t nx, int32_t ny, rtp::DevCamera* out) {
+  v3 up = ld(cam->view_up);
+  if (!(up.x == 0.f && up.y == 1.f && up.z == 0.f)) up = normalize(up);  // SetUp (Camera.cxx:767-776)
+  v3 pos = ld(cam->position);
+  v3 look = normalize(sub(ld(cam->look_at), pos));  // Camera.cxx:908-909
+  const float pi_180f = 0.01745329251994329577f;    // vtkm::Pi_180f()
+  float thx = tanf((cam->fov_y_deg * pi_180f) * .5f);
+  float thy = tanf((cam->fov_y_deg * pi_180f) * .5f);
+  v3 u = normalize(cross(look, up));
+  v3 v = normalize(cross(u, look));
+  st(out->eye, pos);
+  st(out->dx, scl(u, (2 * thx / (float)nx)));
+  st(out->dy, scl(v, (2 * thy / (float)ny)));
+  st(out->nlook, normalize(look));
+}
+
+rtp_status check_render_args(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny, int32_t spp,
+                             int32_t depth) {
+  if (!c || !cam) return fail(RTP_ERR_INVALID_ARGUMENT, "render: NULL argument");
+  if (!c->has_scene) return fail(RTP_ERR_NO_SCENE, "render: rtp_set_scene was not called");
+  if (nx <= 0 || ny <= 0) return fail(RTP_ERR_INVALID_ARGUMENT, "Camera width/height must be greater than zero.");
+  if ((int64_t)nx * ny > INT32_MAX) return fail(RTP_ERR_INVALID_ARGUMENT, "render: canvas too large");
+  if (!(cam->fov_y_deg > 0)) return fail(RTP_ERR_INVALID_ARGUMENT, "Camera feild of view must be greater than zero.");
+  if (cam->fov_y_deg > 180) return fail(RTP_ERR_INVALID_ARGUMENT, "Camera feild of view must be less than 180.");
+  if (spp < 0) return fail(RTP_ERR_INVALID_ARGUMENT, "render: samplecount must be >= 0");
+  // depthcount < 1 makes the reference read emitted[(depth-1)*N] out of range
+  // (MapperPathTracer.cxx:328-331); rejected here.
+  if (depth < 1) return fail(RTP_ERR_INVALID_ARGUMENT, "render: depthcount must be >= 1");
+  return RTP_OK;
+}
+
+rtp_status ensure_hist(rtp_context* c, size_t bytes) {
+  if (bytes <= c->hist_bytes) return RTP_OK;
+  if (c->d_hist) HIP_TRY(hipFree(c->d_hist));
+  c->d_hist = nullptr;
+  c->hist_bytes = 0;
+  HIP_TRY(hipMalloc(&c->d_hist, bytes));
+  c->hist_bytes = bytes;
+  return RTP_OK;
+}
+
+rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny, int32_t spp, int32_t depth,
+                  uint32_t seed_base, int64_t pixel_begin, int64_t npix, const int64_t* d_ids, float* d_out,
+                  uint32_t* d_seed, uint32_t* d_live, hipStream_t stream, double* kernel_ms) {
+  HIP_TRY(hipSetDevice(c->device));
+  rtp::KParams p{};
+  p.scene = c->d_scene;
+  camera_setup(cam, nx, ny, &p.cam);
+  p.nx = nx, p.ny = ny, p.spp = spp, p.depth = depth;
+  p.seed_base = seed_base;
+  p.pixel_begin = pixel_begin;
+  p.pixel_ids = d_ids;
+  p.npix = npix;
+  p.out = d_out;
+  p.seed_out = d_seed;
+  p.live_out = d_live;
+  size_t hist_need = (size_t)(depth > 1 ? depth - 1 : 1) * (size_t)npix * 16;
+  rtp_status rs = ensure_hist(c, hist_need);
+  if (rs != RTP_OK) return rs;
+  p.hist = c->d_hist;
+  if (kernel_ms) HIP_TRY(hipEventRecord(c->ev0, stream));
+  HIP_TRY(rtp_launch_render(&p, stream));
+  if (kernel_ms) {
+    HIP_TRY(hipEventRecord(c->ev1, stream));
+    HIP_TRY(hipEventSynchronize(c->ev1));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    *kernel_ms = ms;
+  }
+  return RTP_OK;
+}
+
+// host-buffer render of an optional pixel list (nullptr: contiguous range)
+rtp_status render_host(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny, int32_t spp, int32_t depth,
+                       uint32_t seed_base, const int64_t* ids, int64_t npix, float* rgba_out,
+                       const rtp_pixel_aux* aux, rtp_stats* stats) {
+  HIP_TRY(hipSetDevice(c->device));
+  if (npix == 0) {
+    if (stats) *stats = rtp_stats{};
+    return RTP_OK;
+  }
+  int64_t* d_ids = nullptr;
+  float* d_out = nullptr;
+  uint32_t *d_seed = nullptr, *d_live = nullptr;
+  rtp_status rs = RTP_OK;
+  double ms = 0;
+  std::vector<uint32_t> live(npix);
+  auto cleanup = [&]() {
+    if (d_ids) hipFree(d_ids);
+    if (d_out) hipFree(d_out);
+    if (d_seed) hipFree(d_seed);
+    if (d_live) hipFree(d_live);
+  };
+  hipError_t e = hipMalloc(&d_out, (size_t)npix * 16);
+  if (e == hipSuccess) e = hipMalloc(&d_live, (size_t)npix * 4);
+  if (e == hipSuccess && aux && aux->final_seed) e = hipMalloc(&d_seed, (size_t)npix * 4);
+  if (e == hipSuccess && ids) {
+    e = hipMalloc(&d_ids, (size_t)npix * 8);
+    if (e == hipSuccess) e = hipMemcpy(d_ids, ids, (size_t)npix * 8, hipMemcpyHostToDevice);
+  }
+  if (e != hipSuccess) {
+    cleanup();
+    return hip_fail(e, "render: device buffers");
+  }
+  rs = launch(c, cam, nx, ny, spp, depth, seed_base, 0, npix, d_ids, d_out, d_seed, d_live, nullptr, &ms);
+  if (rs == RTP_OK) {
+    e = hipMemcpy(rgba_out, d_out, (size_t)npix * 16, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(live.data(), d_live, (size_t)npix * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && d_seed) e = hipMemcpy(aux->final_seed, d_seed, (size_t)npix * 4, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) rs = hip_fail(e, "render: copy back");
+  }
+  cleanup();
+  if (rs != RTP_OK) return rs;
+  if (aux && aux->live_bounces) std::memcpy(aux->live_bounces, live.data(), (size_t)npix * 4);
+  if (stats) {
+    stats->samples = (uint64_t)npix * (uint64_t)spp;
+    uint64_t lb = 0, nan = 0;
+    for (int64_t i = 0; i < npix; i++) {
+      lb += live[i];
+      const float* px = rgba_out + 4 * i;
+      nan += (std::isnan(px[0]) || std::isnan(px[1]) || std::isnan(px[2])) ? 1 : 0;
+    }
+    stats->live_bounces = lb;
+    stats->nan_pixels = nan;
+    stats->kernel_ms = ms;
+  }
+  return RTP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+rtp_status rtp_render(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny, int32_t spp, int32_t depth,
+                      uint32_t seed_base, float* rgba_out, rtp_stats* stats) {
+  rtp_status rs = check_render_args(c, cam, nx, ny, spp, depth);
+  if (rs != RTP_OK) return rs;
+  if (!rgba_out) return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_render: rgba_out is NULL");
+  return render_host(c, cam, nx, ny, spp, depth, seed_base, nullptr, (int64_t)nx * ny, rgba_out, nullptr, stats);
+}
+
+rtp_status rtp_render_pixels(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny, int32_t spp,
+                             int32_t depth, uint32_t seed_base, const int64_t* pixel_ids, int64_t pixel_count,
+                             float* rgba_out, const rtp_pixel_aux* aux, rtp_stats* stats) {
+  rtp_status rs = check_render_args(c, cam, nx, ny, spp, depth);
+  if (rs != RTP_OK) return rs;
+  if (pixel_count < 0 || (pixel_count > 0 && (!pixel_ids || !rgba_out)))
+    return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_render_pixels: bad pixel list / output");
+  const int64_t npx = (int64_t)nx * ny;
+  for (int64_t i = 0; i < pixel_count; i++)
+    if (pixel_ids[i] < 0 || pixel_ids[i] >= npx)
+      return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_render_pixels: pixel id out of range");
+  return render_host(c, cam, nx, ny, spp, depth, seed_base, pixel_ids, pixel_count, rgba_out, aux, stats);
+}
+
+rtp_status rtp_render_device(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny, int32_t spp,
+                             int32_t depth, uint32_t seed_base, int64_t pixel_begin, int64_t pixel_count,
+                             const int64_t* d_pixel_ids, float* d_rgba_out, const rtp_pixel_aux* aux,
+                             void* hip_stream, rtp_stats* stats) {
+  rtp_status rs = check_render_args(c, cam, nx, ny, spp, depth);
+  if (rs != RTP_OK) return rs;
+  if (pixel_count < 0 || (pixel_count > 0 && !d_rgba_out))
+    return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_render_device: bad output");
+  if (!d_pixel_ids && (pixel_begin < 0 || pixel_begin + pixel_count > (int64_t)nx * ny))
+    return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_render_device: pixel range outside the canvas");
+  if (pixel_count == 0) return RTP_OK;
+  double ms = 0;
+  rs = launch(c, cam, nx, ny, spp, depth, seed_base, pixel_begin, pixel_count, d_pixel_ids, d_rgba_out,
+              aux ? aux->final_seed : nullptr, aux ? aux->live_bounces : nullptr, (hipStream_t)hip_stream,
+              stats ? &ms : nullptr);
+  if (rs == RTP_OK && stats) {
+    stats->samples = (uint64_t)pixel_count * (uint64_t)spp;
+    stats->live_bounces = 0;
+    stats->nan_pixels = 0;
+    stats->kernel_ms = ms;
+  }
+  return rs;
+}
+
+rtp_status rtp_eval_primitive(rtp_context* c, int32_t kind, const void* in, void* out, int64_t n) {
+  if (!c || !in || !out || n < 0 || kind < 0 || kind > 3)
+    return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_eval_primitive: bad arguments");
+  if (n == 0) return RTP_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  void *din = nullptr, *dout = nullptr;
+  HIP_TRY(hipMalloc(&din, (size_t)n * 4));
+  hipError_t e = hipMalloc(&dout, (size_t)n * 4);
+  if (e == hipSuccess) e = hipMemcpy(din, in, (size_t)n * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = rtp_launch_eval_primitive(kind, din, dout, n, nullptr);
+  if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)n * 4, hipMemcpyDeviceToHost);
+  hipFree(din);
+  if (dout) hipFree(dout);
+  if (e != hipSuccess) return hip_fail(e, "rtp_eval_primitive");
+  return RTP_OK;
+}
+
+// NormalizeFunctor (main.cc:253-287): de-NaN rgb, then sqrt(c / spp) on all
+// four channels.
+rtp_status rtp_normalize(float* rgba, int64_t n, int32_t spp) {
+  if (!rgba || n < 0) return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_normalize: bad arguments");
+  const float samplecount = (float)spp;
+  for (int64_t i = 0; i < n; i++) {
+    float* px = rgba + 4 * i;
+    for (int k = 0; k < 3; k++)
+      if (!(px[k] == px[k])) px[k] = 0;
+    for (int k = 0; k < 4; k++) px[k] = std::sqrt(px[k] / samplecount);
+  }
+  return RTP_OK;
+}
+
+// save() (main.cc:325-384): P3 header "nx ny 255", one "r g b" line per
+// pixel in buffer order (row 0 = camera bottom), int(255.99*c) unclamped,
+// NaN pixels written as 0.
+rtp_status rtp_write_pnm(const char* path, const float* rgba, int32_t nx, int32_t ny) {
+  if (!path || !rgba || nx <= 0 || ny <= 0) return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_write_pnm: bad arguments");
+  FILE* f = std::fopen(path, "w");
+  if (!f) return fail(RTP_ERR_INVALID_ARGUMENT, std::string("Couldn't save pnm: ") + path);
+  std::fprintf(f, "P3\n%d %d 255\n", nx, ny);
+  const int64_t n = (int64_t)nx * ny;
+  for (int64_t i = 0; i < n; i++) {
+    float c[3] = {rgba[4 * i], rgba[4 * i + 1], rgba[4 * i + 2]};
+    if ((c[0] != c[0]) || (c[1] != c[1]) || (c[2] != c[2])) c[0] = c[1] = c[2] = 0.0f;
+    std::fprintf(f, "%d %d %d\n", (int)(255.99 * c[0]), (int)(255.99 * c[1]), (int)(255.99 * c[2]));
+  }
+  std::fclose(f);
+  return RTP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,167 @@
+// scene_cornell.cpp -- CornellBox::buildDataSet (CornellBox.cpp:141-418) for
+// the C ABI (rtp_cornell_box).  Produces the reference's 89 points, 22 quads
+// (QuadExtractor order, vertex cell skipped), 1 sphere and the material
+// tables, with the reference's float/double arithmetic:
+//   * every coordinate is Vec<float,3>(x) / 555.0 (double divide -> float)
+//   * the small box is rotated by VTK-m's Transform3DRotate(-15 deg, y) in
+//     float, transposed, pre-multiplied by Translate(265,0,295)
+//     (CornellBox::invert, :10-35)
+//   * buildBox's duplicated faces and the y=333 vertex typo are kept.
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/rtp.h"
+
+namespace {
+
+struct SceneStore {
+  std::vector<float> points;
+  std::vector<int32_t> quad_points, quad_mat, quad_tex;
+  std::vector<int32_t> sphere_point, sphere_mat, sphere_tex;
+  std::vector<float> sphere_radius;
+  int32_t mat_type[5] = {0, 0, 0, 1, 2};  // lambertian x3, light, dielectric (:149-154)
+  int32_t tex_type[5] = {0, 1, 2, 3, 0};  // red, white, green, light, dielectric (:156-161)
+  // vec3(0.65, 0.05, 0.05) etc.: double literals converted to float (:144-147)
+  float tex_rgb[12] = {(float)0.65, (float)0.05, (float)0.05, (float)0.73, (float)0.73, (float)0.73,
+                       (float)0.12, (float)0.45, (float)0.15, 15.f,         15.f,         15.f};
+
+  void add_quad(const float p[4][3], int mat, int tex) {
+    const int base = (int)(points.size() / 3);
+    for (int i = 0; i < 4; i++)
+      for (int k = 0; k < 3; k++) points.push_back((float)((double)p[i][k] / 555.0));
+    for (int i = 0; i < 4; i++) quad_points.push_back(base + i);
+    quad_mat.push_back(mat);
+    quad_tex.push_back(tex);
+  }
+};
+
+using P4 = float[4][3];
+
+void rect(P4& p, std::initializer_list<float> v) {
+  auto it = v.begin();
+  for (int i = 0; i < 4; i++)
+    for (int k = 0; k < 3; k++) p[i][k] = *it++;
+}
+
+// CornellBox::invert (CornellBox.cpp:10-35)
+void invert(P4& pts) {
+  const float angle = -15.f;
+  float axis[3] = {0.f, 1.f, 0.f};
+  {  // vtkm::Normal
+    float r = 1 / std::sqrt(axis[0] * axis[0] + axis[1] * axis[1] + axis[2] * axis[2]);
+    for (float& a : axis) a = a * r;
+  }
+  const float rad = 0.01745329251994329577f * angle;  // Pi_180<float>() * angle
+  const float sn = std::sin(rad), cs = std::cos(rad);
+  const float x = axis[0], y = axis[1], z = axis[2];
+  float R[4][4] = {{x * x * (1 - cs) + cs, x * y * (1 - cs) - z * sn, x * z * (1 - cs) + y * sn, 0},
+                   {y * x * (1 - cs) + z * sn, y * y * (1 - cs) + cs, y * z * (1 - cs) - x * sn, 0},
+                   {z * x * (1 - cs) - y * sn, z * y * (1 - cs) + x * sn, z * z * (1 - cs) + cs, 0},
+                   {0, 0, 0, 1}};
+  float T[4][4] = {{1, 0, 0, 265}, {0, 1, 0, 0}, {0, 0, 1, 295}, {0, 0, 0, 1}};
+  float M[4][4];
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) {
+      float acc = T[i][0] * R[j][0];  // right factor is R^T: (R^T)[k][j] = R[j][k]
+      for (int k = 1; k < 4; k++) acc = acc + T[i][k] * R[j][k];
+      M[i][j] = acc;
+    }
+  for (auto& pt : pts) {
+    const float v[4] = {pt[0], pt[1], pt[2], 1.f};
+    float o[3];
+    for (int i = 0; i < 3; i++) o[i] = M[i][0] * v[0] + M[i][1] * v[1] + M[i][2] * v[2] + M[i][3] * v[3];
+    std::memcpy(pt, o, sizeof(o));
+  }
+}
+
+// CornellBox::buildBox (:63-139): near, far, top, near (dup), far (dup)
+void box(SceneStore& s, const float n[3], const float f[3]) {
+  P4 p;
+  rect(p, {n[0], n[1], n[2], f[0], n[1], n[2], f[0], f[1], n[2], n[0], f[1], n[2]});
+  s.add_quad(p, 1, 1);
+  rect(p, {n[0], n[1], f[2], f[0], n[1], f[2], f[0], f[1], f[2], n[0], f[1], f[2]});
+  s.add_quad(p, 1, 1);
+  rect(p, {n[0], f[1], n[2], f[0], f[1], n[2], f[0], f[1], f[2], n[0], f[1], f[2]});
+  s.add_quad(p, 1, 1);
+  rect(p, {n[0], n[1], n[2], f[0], n[1], n[2], f[0], f[1], n[2], n[0], f[1], n[2]});
+  s.add_quad(p, 1, 1);
+  rect(p, {n[0], n[1], f[2], f[0], n[1], f[2], f[0], f[1], f[2], n[0], f[1], f[2]});
+  s.add_quad(p, 1, 1);
+}
+
+void build(SceneStore& s, int variant) {
+  P4 p;
+  rect(p, {555, 0, 0, 555, 555, 0, 555, 555, 555, 555, 0, 555});  // green wall (:175-186)
+  s.add_quad(p, 2, 2);
+  rect(p, {0, 0, 0, 0, 555, 0, 0, 555, 555, 0, 0, 555});  // red wall (:189-200)
+  s.add_quad(p, 0, 0);
+  rect(p, {213, 554, 227, 343, 554, 227, 343, 554, 332, 213, 554, 332});  // light (:204-215)
+  s.add_quad(p, 3, 3);
+  rect(p, {0, 555, 0, 555, 555, 0, 555, 555, 555, 0, 555, 555});  // ceiling
+  s.add_quad(p, 1, 1);
+  rect(p, {0, 0, 0, 555, 0, 0, 555, 0, 555, 0, 0, 555});  // floor
+  s.add_quad(p, 1, 1);
+  rect(p, {0, 0, 555, 555, 0, 555, 555, 555, 555, 0, 555, 555});  // back wall
+  s.add_quad(p, 1, 1);
+  const std::initializer_list<float> small_box[6] = {
+      {0, 0, 165, 165, 0, 165, 165, 330, 165, 0, 330, 165},  {0, 0, 0, 165, 0, 0, 165, 330, 0, 0, 330, 0},
+      {165, 0, 0, 165, 330, 0, 165, 330, 165, 165, 0, 165},  {0, 0, 0, 0, 330, 0, 0, 330, 165, 0, 0, 165},
+      {0, 333, 0, 165, 330, 0, 165, 330, 165, 0, 330, 165}, {0, 0, 0, 165, 0, 0, 165, 0, 165, 0, 0, 165}};
+  for (const auto& r : small_box) {
+    rect(p, r);
+    invert(p);
+    s.add_quad(p, 1, 1);
+  }
+  // glass sphere vertex cell (:357-365); the extractor radius is 90/555.0
+  const float c[3] = {variant == 1 ? 190.f : -335.f, 90.f, variant == 1 ? 190.f : 290.f};
+  s.sphere_point.push_back((int32_t)(s.points.size() / 3));
+  for (float v : c) s.points.push_back((float)((double)v / 555.0));
+  s.sphere_radius.push_back((float)(90 / 555.0));
+  s.sphere_mat.push_back(4);
+  s.sphere_tex.push_back(0);
+  const float rad = 90;
+  const float bc[3] = {135, 90, 290};
+  const float n1[3] = {bc[0] - rad, 0, bc[2] - rad}, f1[3] = {bc[0] + rad, 180, bc[2] + rad};
+  box(s, n1, f1);
+  const float n2[3] = {50, 0, 50}, f2[3] = {450, 100, 100};
+  box(s, n2, f2);
+}
+
+SceneStore g_store[2];
+std::once_flag g_once[2];
+
+}  // namespace
+
+extern "C" rtp_status rtp_cornell_box(int32_t variant, rtp_scene_desc* out) {
+  if (!out || variant < 0 || variant > 1) return RTP_ERR_INVALID_ARGUMENT;
+  std::call_once(g_once[variant], [variant] { build(g_store[variant], variant); });
+  const SceneStore& s = g_store[variant];
+  std::memset(out, 0, sizeof(*out));
+  out->points = s.points.data();
+  out->n_points = (int32_t)(s.points.size() / 3);
+  out->quad_points = s.quad_points.data();
+  out->quad_mat = s.quad_mat.data();
+  out->quad_tex = s.quad_tex.data();
+  out->n_quads = (int32_t)s.quad_mat.size();
+  out->sphere_point = s.sphere_point.data();
+  out->sphere_radius = s.sphere_radius.data();
+  out->sphere_mat = s.sphere_mat.data();
+  out->sphere_tex = s.sphere_tex.data();
+  out->n_spheres = (int32_t)s.sphere_point.size();
+  out->mat_type = s.mat_type;
+  out->n_mat = 5;
+  out->tex_type = s.tex_type;
+  out->n_tex_type = 5;
+  out->tex_rgb = s.tex_rgb;
+  out->n_tex = 4;
+  // MapperPathTracer.cxx:141-148
+  out->light_quad_points[0] = 8;
+  out->light_quad_points[1] = 9;
+  out->light_quad_points[2] = 10;
+  out->light_quad_points[3] = 11;
+  out->light_sphere_point = 4 * 12;
+  out->ior = 1.5f;
+  return RTP_OK;
+}

@@ -1,0 +1,43 @@
+"""Shared helpers for the parity tests."""
+from __future__ import annotations
+
+import numpy as np
+
+
+def same_bits_or_both_nan(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """Elementwise: identical float32 bit patterns, or both NaN (the NaN payload
+    differs between x86 SSE and CDNA and carries no information here)."""
+    a = np.asarray(a, dtype=np.float32)
+    b = np.asarray(b, dtype=np.float32)
+    return (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+
+
+def assert_render_equal(got, want, what=""):
+    """got/want: (rgba, seeds, live).  rgb sums bit-exact (NaN-aware), the
+    final RNG state and the live-bounce count exact."""
+    g_rgba, g_seed, g_live = got
+    w_rgba, w_seed, w_live = want
+    ok = same_bits_or_both_nan(g_rgba[:, :3], w_rgba[:, :3]).all(axis=1)
+    bad = np.flatnonzero(~ok)
+    assert bad.size == 0, (
+        f"{what}: {bad.size} pixels differ, first {bad[:8].tolist()}: got {g_rgba[bad[:4]].tolist()} "
+        f"want {w_rgba[bad[:4]].tolist()}"
+    )
+    if g_seed is not None and w_seed is not None:
+        sb = np.flatnonzero(np.asarray(g_seed) != np.asarray(w_seed))
+        assert sb.size == 0, f"{what}: final RNG state differs at {sb[:8].tolist()}"
+    if g_live is not None and w_live is not None:
+        lb = np.flatnonzero(np.asarray(g_live) != np.asarray(w_live))
+        assert lb.size == 0, f"{what}: live-bounce count differs at {lb[:8].tolist()}"
+
+
+def rmse_normalized(a_sum: np.ndarray, b_sum: np.ndarray, spp: int) -> float:
+    """Per-pixel RMSE of the NormalizeFunctor outputs (main.cc:253-287)."""
+
+    def norm(x):
+        x = np.array(x[:, :3], dtype=np.float32)
+        x[np.isnan(x)] = 0
+        return np.sqrt(x / np.float32(spp))
+
+    d = norm(a_sum).astype(np.float64) - norm(b_sum).astype(np.float64)
+    return float(np.sqrt(np.mean(d * d)))

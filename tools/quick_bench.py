@@ -1,0 +1,29 @@
+"""Quick C2-geometry timing of the HIP render kernel (development tool)."""
+import argparse, json, os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+import raytracingtherestofyourlife_amd as rtp
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--nx", type=int, default=800)
+ap.add_argument("--ny", type=int, default=800)
+ap.add_argument("--spp", type=int, default=50)
+ap.add_argument("--depth", type=int, default=50)
+ap.add_argument("--reps", type=int, default=2)
+a = ap.parse_args()
+dev = rtp.Device(0)
+dev.set_cornell_box(0)
+cam = rtp.default_camera()
+n = a.nx * a.ny
+out = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
+live = torch.zeros(n, dtype=torch.int32, device="cuda")
+s = torch.cuda.current_stream().cuda_stream
+for r in range(a.reps):
+    t = time.time()
+    st = dev.render_device(cam, a.nx, a.ny, a.spp, a.depth, out.data_ptr(), stream=s, live_ptr=live.data_ptr(), timed=True)
+    torch.cuda.synchronize()
+    wall = time.time() - t
+    L = live.to(torch.int64).sum().item() / (n * a.spp)
+    print(json.dumps(dict(rep=r, kernel_ms=st.kernel_ms, wall_s=wall, msamples_per_s=n * a.spp / (st.kernel_ms / 1e3) / 1e6,
+                          live_per_sample=L, nan_px=int(torch.isnan(out[:, :3]).any(1).sum().item()))), flush=True)
