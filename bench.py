@@ -1,0 +1,232 @@
+"""Benchmark of the path-tracing hot path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+One step = one full render of the C2 workload on every rank: Cornell Box,
+800x800 pixels per GPU, 1000 spp, depth 50 (BASELINE.json configs[1]).
+N > 1 (launched by torch.distributed.run, one process per GPU): weak scaling
+by image tiles -- the canvas is 800 x (800*N), 16x16 tiles are dealt to the
+ranks round-robin (every rank renders 640,000 pixels), and the float4
+framebuffer is summed to rank 0 with ONE RCCL reduce per step (exact: every
+pixel is non-zero on exactly one rank).
+
+Rank 0 prints one JSON line.  `value` = all ranks' samples / max-over-ranks
+wall time of the K timed steps.  `roofline` prices the render kernel with the
+SoA byte model of SURVEY.md 8(d) (56 + 88*L bytes per sample, L = mean live
+bounces per sample, counted by the kernel) against the 8 TB/s HBM peak;
+`cpu_baseline` times the oracle's stage-structured restatement on a bounded
+sample of the same workload on this host (1 thread).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Msamples/sec (whole node), Cornell Box 800×800×1000spp; per-pixel RMSE vs ref"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+TILE = 16
+
+
+def tile_pixels(nx: int, ny: int, rank: int, world: int) -> np.ndarray:
+    """Pixel ids of the 16x16 tiles owned by `rank` (tile t -> rank t % world),
+    each tile in row-major order (a 64-lane wave covers a 16x4 block)."""
+    tx, ty = nx // TILE, ny // TILE
+    assert tx * TILE == nx and ty * TILE == ny, "canvas must be a multiple of the tile size"
+    tiles = np.arange(tx * ty)
+    mine = tiles[tiles % world == rank]
+    oy, ox = np.divmod(mine, tx)
+    ly, lx = np.divmod(np.arange(TILE * TILE), TILE)
+    rows = (oy[:, None] * TILE + ly[None, :]).astype(np.int64)
+    cols = (ox[:, None] * TILE + lx[None, :]).astype(np.int64)
+    return (rows * nx + cols).reshape(-1)
+
+
+def cpu_baseline(budget_s: float, nx: int, ny: int, depth: int) -> dict:
+    """Oracle stage-structured SoA pass sequence (the reference's cost model),
+    1 thread, spp=1, on a band of image rows sized to ~budget_s."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_ctypes as oc
+
+    oc.build()
+    sc = oc.cornell_box(0)
+    cam = oc.camera_setup(nx, ny)
+    mid = ny // 2
+    rows = 8
+    t = time.perf_counter()
+    oc.render_soa(sc, cam, nx, ny, 1, depth, row_begin=mid - rows // 2, row_end=mid + rows // 2, nthreads=1)
+    probe = time.perf_counter() - t
+    rows = int(max(8, min(ny, rows * budget_s / max(probe, 1e-3))))
+    r0 = max(0, mid - rows // 2)
+    r1 = min(ny, r0 + rows)
+    t = time.perf_counter()
+    oc.render_soa(sc, cam, nx, ny, 1, depth, row_begin=r0, row_end=r1, nthreads=1)
+    dt = time.perf_counter() - t
+    samples = (r1 - r0) * nx
+    return {
+        "value": samples / dt / 1e6,
+        "unit": "Msamples/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"C2 camera {nx}x{ny}, rows {r0}-{r1} ({samples} pixels), 1 spp, depth {depth}, "
+                  f"stage-structured SoA oracle (cost/sample independent of spp), {dt:.1f}s",
+    }
+
+
+def load_traffic(path: str, cfg: dict):
+    """Per-launch HBM bytes measured by rocprofv3 --pmc for this config (or None)."""
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if all(t.get(k) == v for k, v in cfg.items()):
+        return t.get("hbm_bytes_per_launch")
+    return None
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--nx", type=int, default=800)
+    ap.add_argument("--ny", type=int, default=800, help="rows per GPU (canvas is nx x ny*N)")
+    ap.add_argument("--spp", type=int, default=1000)
+    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work (0: skip)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c2.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import raytracingtherestofyourlife_amd as rtp
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    nx, ny = args.nx, args.ny * world
+    ids_np = tile_pixels(nx, ny, rank, world)
+    npix = ids_np.size
+    dev = rtp.Device(local)
+    dev.set_cornell_box(0)
+    cam = rtp.default_camera()
+    ids = torch.from_numpy(ids_np).cuda()
+    out = torch.empty((npix, 4), dtype=torch.float32, device="cuda")
+    canvas = torch.zeros((nx * ny, 4), dtype=torch.float32, device="cuda")
+    live = torch.zeros(npix, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def step(count_live: bool = False):
+        dev.render_device(cam, nx, ny, args.spp, args.depth, out.data_ptr(), pixel_count=npix,
+                          pixel_ids_ptr=ids.data_ptr(), stream=stream.cuda_stream,
+                          live_ptr=live.data_ptr() if count_live else 0)
+        canvas.zero_()
+        canvas.index_copy_(0, ids, out)
+        if world > 1:
+            dist.reduce(canvas, dst=0, op=dist.ReduceOp.SUM)
+
+    for i in range(args.warmup):
+        step(count_live=(i == 0))
+    if args.warmup == 0:
+        step(count_live=True)
+    torch.cuda.synchronize()
+    live_total = int(live.to(torch.int64).sum().item())
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        # kernel duration bracketed on the stream the kernel is launched on
+        ev[k][0].record(stream)
+        dev.render_device(cam, nx, ny, args.spp, args.depth, out.data_ptr(), pixel_count=npix,
+                          pixel_ids_ptr=ids.data_ptr(), stream=stream.cuda_stream)
+        ev[k][1].record(stream)
+        canvas.zero_()
+        canvas.index_copy_(0, ids, out)
+        if world > 1:
+            dist.reduce(canvas, dst=0, op=dist.ReduceOp.SUM)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if args.steps else float("nan")
+    if world > 1:
+        t = torch.tensor([elapsed, live_total], dtype=torch.float64, device="cuda")
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        tot = t.clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        elapsed = float(mx[0].item())
+        live_all = float(tot[1].item())
+    else:
+        live_all = float(live_total)
+
+    samples_rank = npix * args.spp
+    samples_all = samples_rank * world
+    value = samples_all * args.steps / elapsed / 1e6
+    L = live_all / samples_all
+    bytes_per_sample = 56.0 + 88.0 * L
+    achieved = samples_rank * bytes_per_sample / (kernel_ms / 1e3) / 1e9
+    cfg = {"nx": nx, "ny": args.ny, "spp": args.spp, "depth": args.depth}
+    traffic = load_traffic(args.traffic_json, cfg)
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and args.cpu_budget > 0:
+            cpu = cpu_baseline(args.cpu_budget, args.nx, args.ny, args.depth)
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / max(args.steps, 1) * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32 (f64 mixture/pdf islands)",
+            "data": "synthetic: the reference's deterministic Cornell Box scene and camera (main.cc:616-622), "
+                    "seed = pixel index",
+            "config": {
+                "workload": "C2: Cornell Box 800x800 per GPU, 1000 spp, depth 50",
+                "nx": nx, "ny": ny, "spp": args.spp, "depth": args.depth,
+                "pixels_per_gpu": npix, "shard": f"{TILE}x{TILE} tiles round-robin, 1 RCCL reduce/step",
+                "live_bounces_per_sample": round(L, 6),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 3),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 6),
+                "traffic": traffic,
+                "kernel_ms": round(kernel_ms, 3),
+                "bytes_per_sample_model": round(bytes_per_sample, 3),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -135,14 +135,15 @@ rtp_status rtp_render_pixels(rtp_context* ctx, const rtp_camera* cam, int32_t nx
 rtp_status rtp_normalize(float* rgba, int64_t n_pixels, int32_t spp);
 rtp_status rtp_write_pnm(const char* path, const float* rgba, int32_t nx, int32_t ny);
 
-/* CornellBox::buildDataSet.  variant 0: the reference scene; variant 1:
- * sphere moved to (190,90,190) so the dielectric is visible.  The returned
- * descriptor points into library-owned static storage. */
+/* CornellBox::buildDataSet.  variant 0: the reference scene (glass sphere
+ * outside the box); 1: sphere at (190,90,190) (notebook cell 2; overlaps the
+ * tall box); 2: sphere floating at (440,200,150), clear of the boxes.  The
+ * returned descriptor points into library-owned static storage. */
 rtp_status rtp_cornell_box(int32_t variant, rtp_scene_desc* out);
 
 /* Diagnostics: evaluate a device primitive elementwise (tests only).
  * kind 0: glibc-exact sinf port, 1: cosf port, 2: 1/sqrtf(x) (RMagnitude),
- * 3: wang32 (bit pattern in/out), 4: which(hash) thresholds. */
+ * 3: wang32 (bit pattern in/out).  in/out: n 4-byte elements, host memory. */
 rtp_status rtp_eval_primitive(rtp_context* ctx, int32_t kind, const void* in, void* out, int64_t n);
 
 #ifdef __cplusplus

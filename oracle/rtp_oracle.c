@@ -420,6 +420,7 @@ void rtpo_cornell_box(int32_t variant, rtpo_scene* s) {
   /* sphere vertex cell (:357-365) */
   float scx = -335, scy = 90, scz = 290;
   if (variant == 1) scx = 190, scy = 90, scz = 190;
+  if (variant == 2) scx = 440, scy = 200, scz = 150;
   const float sphere_radii = 90;
   s->sphere_point[0] = s->n_points;
   cb_push_point(s, d555(scx), d555(scy), d555(scz));
@@ -1074,4 +1075,25 @@ void rtpo_normalize(float* rgba, int64_t n, int32_t spp) {
       if (!(c[k] == c[k])) c[k] = 0;
     for (int k = 0; k < 4; k++) c[k] = sqrtf(c[k] / samplecount);
   }
+}
+
+/* Test helper: compare the sinf/cosf restatement with this host's libm on
+ * every stride-th float in [lo, hi] (bit patterns).  Returns the mismatch
+ * count; *checked receives the number of floats compared. */
+int64_t rtpo_check_sincos_vs_libm(float lo, float hi, uint32_t stride, int64_t* checked) {
+  uint32_t a, b;
+  memcpy(&a, &lo, 4);
+  memcpy(&b, &hi, 4);
+  int64_t bad = 0, n = 0;
+  if (stride == 0) stride = 1;
+  for (uint64_t u = a; u <= b; u += stride) {
+    uint32_t uu = (uint32_t)u;
+    float f;
+    memcpy(&f, &uu, 4);
+    float s0 = rtpo_sinf(f), s1 = sinf(f), c0 = rtpo_cosf(f), c1 = cosf(f);
+    if (memcmp(&s0, &s1, 4) != 0 || memcmp(&c0, &c1, 4) != 0) bad++;
+    n++;
+  }
+  if (checked) *checked = n;
+  return bad;
 }

@@ -63,7 +63,10 @@ void rtpo_camera_setup(const float pos[3], const float look_at[3], const float u
 /* variant 0: reference scene (CornellBox.cpp:141-418, glass sphere at x=-335,
  *            outside the box).
  * variant 1: same, sphere moved to (190,90,190) (notebook cell 2) so the
- *            dielectric path is exercised. */
+ *            dielectric path is exercised (it overlaps the tall box: most
+ *            pixels NaN-poison, a stress case for the NaN semantics).
+ * variant 2: sphere floating at (440,200,150), clear of every box (a clean
+ *            visible glass sphere). */
 void rtpo_cornell_box(int32_t variant, rtpo_scene* out);
 
 /* Scalar per-pixel render of an arbitrary pixel subset (pixels are fully
@@ -93,6 +96,7 @@ float rtpo_randf(uint32_t* seed);
 float rtpo_sinf(float x);
 float rtpo_cosf(float x);
 int32_t rtpo_which(uint32_t hash_value);
+int64_t rtpo_check_sincos_vs_libm(float lo, float hi, uint32_t stride, int64_t* checked);
 
 #ifdef __cplusplus
 }

@@ -77,6 +77,14 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
             raise RuntimeError(f"{LIB_PATH} is missing; run raytracingtherestofyourlife_amd/build.py")
         from . import build as _build
         _build.build()
+    # One HIP runtime per process: torch bundles a libamdhip64 with the same
+    # soname (libamdhip64.so.7) as /opt/rocm's.  Loading torch's first makes
+    # librtp.so bind to it (soname match), so torch streams/allocations and
+    # our launches share one runtime.  Without torch, /opt/rocm's is used.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     L.rtp_last_error.restype = ctypes.c_char_p
     L.rtp_abi_version.restype = ctypes.c_int32

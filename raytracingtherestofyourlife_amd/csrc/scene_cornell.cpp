@@ -115,7 +115,9 @@ void build(SceneStore& s, int variant) {
     s.add_quad(p, 1, 1);
   }
   // glass sphere vertex cell (:357-365); the extractor radius is 90/555.0
-  const float c[3] = {variant == 1 ? 190.f : -335.f, 90.f, variant == 1 ? 190.f : 290.f};
+  float c[3] = {-335.f, 90.f, 290.f};
+  if (variant == 1) c[0] = 190.f, c[1] = 90.f, c[2] = 190.f;  // notebook cell 2 position
+  if (variant == 2) c[0] = 440.f, c[1] = 200.f, c[2] = 150.f;  // floating, clear of the boxes
   s.sphere_point.push_back((int32_t)(s.points.size() / 3));
   for (float v : c) s.points.push_back((float)((double)v / 555.0));
   s.sphere_radius.push_back((float)(90 / 555.0));
@@ -129,13 +131,13 @@ void build(SceneStore& s, int variant) {
   box(s, n2, f2);
 }
 
-SceneStore g_store[2];
-std::once_flag g_once[2];
+SceneStore g_store[3];
+std::once_flag g_once[3];
 
 }  // namespace
 
 extern "C" rtp_status rtp_cornell_box(int32_t variant, rtp_scene_desc* out) {
-  if (!out || variant < 0 || variant > 1) return RTP_ERR_INVALID_ARGUMENT;
+  if (!out || variant < 0 || variant > 2) return RTP_ERR_INVALID_ARGUMENT;
   std::call_once(g_once[variant], [variant] { build(g_store[variant], variant); });
   const SceneStore& s = g_store[variant];
   std::memset(out, 0, sizeof(*out));

@@ -86,9 +86,12 @@ def test_c1_full_image_bit_exact(oracle, device, rtp):
 
 
 def test_visible_glass_sphere_bit_exact(oracle, device, rtp):
-    """Dielectric path (sphere moved into view, notebook cell 2 position)."""
+    """Dielectric path: variant 2 (clean glass sphere) and variant 1 (notebook
+    cell 2 position, overlapping a box: NaN-poisoning stress case)."""
+    got, want = _render_both(oracle, device, rtp, 2, 96, 96, 32, 20)
+    assert_render_equal(got, want, "glass sphere v2")
     got, want = _render_both(oracle, device, rtp, 1, 96, 96, 16, 12)
-    assert_render_equal(got, want, "glass sphere")
+    assert_render_equal(got, want, "glass sphere v1")
     # the dielectric really was exercised: the two scenes differ
     other = device.render_pixels(rtp.default_camera(), 96, 96, 16, 12, np.arange(96 * 96))[0]
     device.set_cornell_box(0)

@@ -1,0 +1,92 @@
+"""Generate the committed golden fixtures under tests/golden/ from the CPU
+oracle (oracle/rtp_oracle.c).  The reference itself cannot be built here (it
+needs VTK-m), so these are known-answer vectors of the restatement; see
+DESIGN.md "Parity".
+
+    python tools/make_golden.py            # all fixtures (~1-2 min, 8 cores)
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import oracle_ctypes as oc  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden")
+
+
+def hexf(a):
+    return [float(x).hex() for x in np.asarray(a, dtype=np.float32).reshape(-1)]
+
+
+def subset(n_total, k, seed):
+    rng = np.random.default_rng(seed)
+    return np.sort(rng.choice(n_total, size=k, replace=False)).astype(np.int64)
+
+
+def render_fixture(name, variant, nx, ny, spp, depth, pixels=None, seed_base=0, camera=None):
+    t = time.time()
+    sc = oc.cornell_box(variant)
+    cam = oc.camera_setup(nx, ny, **(camera or {}))
+    if pixels is None:
+        pixels = np.arange(nx * ny, dtype=np.int64)
+    rgba, seeds, live = oc.render_pixels(sc, cam, nx, ny, spp, depth, pixels, seed_base=seed_base)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), variant=variant, nx=nx, ny=ny, spp=spp, depth=depth,
+                        seed_base=seed_base, camera=cam, pixels=pixels, rgb=rgba[:, :3], final_seed=seeds,
+                        live=live)
+    print(f"{name}: {pixels.size} px x {spp} spp x depth {depth}: {time.time() - t:.1f}s, "
+          f"L={live.sum() / (pixels.size * spp):.4f}, nan_px={int(np.isnan(rgba[:, :3]).any(1).sum())}")
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    L = oc.lib()
+    # --- known answers -------------------------------------------------
+    kat = {"wang32": {str(x): oc.wang32(x) for x in (0, 1, 61, 639999, 2**31, 2**32 - 1)}}
+    kat["randf"] = {str(s): [float(v).hex() for v in oc.randf_stream(s, 8)[0]] for s in (0, 1, 639999)}
+    lo = 0
+    thr = []
+    for w in (2, 3):
+        a, b = 0, 1 << 32
+        while a < b:
+            m = (a + b) // 2
+            if L.rtpo_which(m) >= w:
+                b = m
+            else:
+                a = m + 1
+        thr.append(a)
+    kat["which_thresholds"] = thr
+    sc = oc.cornell_box(0)
+    kat["scene_points_hex"] = hexf(sc.points_np())
+    kat["scene_quad_ids"] = sc.quad_ids_np().tolist()
+    kat["camera_800x800_hex"] = hexf(oc.camera_setup(800, 800))
+    kat["camera_200x200_hex"] = hexf(oc.camera_setup(200, 200))
+    kat["camera_1920x1080_hex"] = hexf(oc.camera_setup(1920, 1080))
+    phis = np.float32([0.0, 0.5, 0.7853982, 1.0, 2.0, 3.1415927, 4.0, 5.5, 6.2831855])
+    kat["sinf"] = {float(p).hex(): float(L.rtpo_sinf(float(p))).hex() for p in phis}
+    kat["cosf"] = {float(p).hex(): float(L.rtpo_cosf(float(p))).hex() for p in phis}
+    with open(os.path.join(OUT, "kat.json"), "w") as f:
+        json.dump(kat, f, indent=1)
+    # --- renders ---------------------------------------------------------
+    # C1 (BASELINE configs[0]): full image
+    render_fixture("c1_full", 0, 200, 200, 10, 10)
+    # C2 geometry at full spp/depth on a fixed 4096-pixel subset
+    render_fixture("c2_subset", 0, 800, 800, 1000, 50, pixels=subset(800 * 800, 4096, 2))
+    # C4 geometry (1920x1080, 4096 spp, depth 50) on a 256-pixel subset
+    render_fixture("c4_subset", 0, 1920, 1080, 4096, 50, pixels=subset(1920 * 1080, 256, 4))
+    # dielectric visible: variant 1 (overlapping, NaN-heavy) and variant 2 (clean)
+    render_fixture("glass_subset", 1, 256, 256, 64, 50, pixels=subset(256 * 256, 2048, 6))
+    render_fixture("glass2_subset", 2, 256, 256, 256, 50, pixels=subset(256 * 256, 2048, 9))
+    # sample-batch shard stream: seed_base = k*N for shard k = 3 of C5 geometry
+    render_fixture("c5_shard3_subset", 0, 3840, 2160, 16, 50, pixels=subset(3840 * 2160, 512, 8),
+                   seed_base=(3 * 3840 * 2160) % (1 << 32))
+
+
+if __name__ == "__main__":
+    main()
