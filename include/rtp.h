@@ -146,6 +146,21 @@ rtp_status rtp_cornell_box(int32_t variant, rtp_scene_desc* out);
  * 3: wang32 (bit pattern in/out).  in/out: n 4-byte elements, host memory. */
 rtp_status rtp_eval_primitive(rtp_context* ctx, int32_t kind, const void* in, void* out, int64_t n);
 
+/* Diagnostics: with RTP_DEBUG_STATS=1 in the environment the render kernel
+ * records per-wave counters (bounce steps, live lanes, fast-forward batches,
+ * shader-clock cycles per phase); this sums them over waves into out[0..n_out)
+ * (out[8], if requested, = the longest wave lifetime) and returns the wave
+ * count of the last such launch (0 if none). */
+int32_t rtp_debug_counters(rtp_context* ctx, uint64_t* out, int32_t n_out);
+
+/* Diagnostics: exhaustively compare a fast device arithmetic sequence with the
+ * IEEE operation for every float bit pattern in [lo_bits, hi_bits].  kind 0:
+ * rcp (v_rcp + 1 Newton step) vs 1.0f/x; 1: rcp + remainder correction; 2:
+ * fast sqrt vs sqrtf; 3/4: 1/sqrt with rcp kind 0/1.  *mismatches = count,
+ * *first_bad = smallest mismatching bit pattern (0xffffffff if none). */
+rtp_status rtp_verify_fast_math(rtp_context* ctx, int32_t kind, uint32_t lo_bits, uint32_t hi_bits,
+                                uint64_t* mismatches, uint32_t* first_bad);
+
 #ifdef __cplusplus
 }
 #endif

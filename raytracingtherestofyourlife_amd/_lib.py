@@ -9,7 +9,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librtp.so")
+LIB_PATH = os.environ.get("RTP_LIB_PATH") or os.path.join(_HERE, "librtp.so")  # override: experiments only
 
 RTP_OK = 0
 RTP_ERR_INVALID_ARGUMENT = -1
@@ -54,7 +54,7 @@ class RtpPixelAux(ctypes.Structure):
 EXPORTED_SYMBOLS = [
     "rtp_last_error", "rtp_abi_version", "rtp_create", "rtp_destroy", "rtp_set_scene", "rtp_render",
     "rtp_render_device", "rtp_render_pixels", "rtp_normalize", "rtp_write_pnm", "rtp_cornell_box",
-    "rtp_eval_primitive",
+    "rtp_eval_primitive", "rtp_debug_counters", "rtp_verify_fast_math",
 ]
 
 
@@ -106,6 +106,9 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.rtp_write_pnm.argtypes = [ctypes.c_char_p, f32p, ctypes.c_int32, ctypes.c_int32]
     L.rtp_cornell_box.argtypes = [ctypes.c_int32, ctypes.POINTER(RtpSceneDesc)]
     L.rtp_eval_primitive.argtypes = [vp, ctypes.c_int32, vp, vp, ctypes.c_int64]
+    L.rtp_debug_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32]
+    L.rtp_verify_fast_math.argtypes = [vp, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32,
+                                       ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]
     for name in EXPORTED_SYMBOLS:
         if name not in ("rtp_last_error", "rtp_abi_version", "rtp_destroy"):
             getattr(L, name).restype = ctypes.c_int32

@@ -31,16 +31,80 @@ RTP_DEV f3 neg(f3 a) { return mk(-a.x, -a.y, -a.z); }
 RTP_DEV float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 // vtkm::Cross without VTKM_FMA (default x86-64 build)
 RTP_DEV f3 cross(f3 a, f3 b) { return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
-// vtkm::RMagnitude on the CPU build: 1 / sqrt(x.x)
-RTP_DEV float rmag(f3 a) { return 1.0f / __builtin_sqrtf(dot(a, a)); }
-RTP_DEV float magn(f3 a) { return __builtin_sqrtf(dot(a, a)); }
-RTP_DEV f3 unit_vector(f3 a) { return scl(a, rmag(a)); }  // vec3.h:38-42
 RTP_DEV f3 de_nan(f3 c) {                                 // PdfWorklet.h:38-44
   if (!(c.x == c.x)) c.x = 0;
   if (!(c.y == c.y)) c.y = 0;
   if (!(c.z == c.z)) c.z = 0;
   return c;
 }
+
+// ------------------------------------------------- fast exact arithmetic ---
+// Candidate short sequences for RN(1/x) and RN(sqrt(x)) without the scaling
+// and special-case steps of the general IEEE lowering.  They are used only
+// where rtp_verify_fast_math (exhaustive, every float of the stated range, on
+// the device) shows them bit-identical to the IEEE operation.
+RTP_DEV float rcp_nr1(float x) {  // v_rcp_f32 + one Newton step (fused)
+  float r = __builtin_amdgcn_rcpf(x);
+  float e = __builtin_fmaf(-x, r, 1.0f);
+  return __builtin_fmaf(e, r, r);
+}
+RTP_DEV float rcp_nr2(float x) {  // + Markstein remainder correction
+  float r = __builtin_amdgcn_rcpf(x);
+  float e = __builtin_fmaf(-x, r, 1.0f);
+  r = __builtin_fmaf(e, r, r);
+  float q = r;
+  float rem = __builtin_fmaf(-x, q, 1.0f);
+  return __builtin_fmaf(rem, r, q);
+}
+RTP_DEV float sqrt_fast(float x) {  // v_sqrt_f32 + residual-based rounding fix (normal x)
+  float s = __builtin_amdgcn_sqrtf(x);
+  float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
+  float rd = __builtin_fmaf(-sd, s, x), ru = __builtin_fmaf(-su, s, x);
+  s = (rd <= 0.0f) ? sd : s;
+  s = (ru > 0.0f) ? su : s;
+  return s;
+}
+
+// ------------------------------------------------------ exact wrappers ---
+// rcp_nr1(x) == 1.0f/x and sqrt_fast(x) == sqrtf(x) bit for bit for every
+// float with |x| in [2^-40, 2^40] (exhaustive device check, tools/
+// verify_fast_math.py and tests/test_gpu_fast_math.py); outside that range
+// (zero, denormal-scale, huge, Inf, NaN) the IEEE operation is used.
+RTP_DEV bool fast_range(float x) { return fabsf(x) >= 0x1p-40f && fabsf(x) <= 0x1p40f; }
+// The IEEE fallback sits behind a wave-uniform branch (ballot) holding an
+// empty volatile asm, so the compiler cannot speculate it into the common
+// path (it otherwise computes both and selects).
+RTP_DEV float rcp_exact(float x) {  // 1.0f / x
+  float r = rcp_nr1(x);
+  const bool slow = !fast_range(x);
+  if (__ballot(slow)) {
+    asm volatile("");
+    if (slow) r = 1.0f / x;
+  }
+  return r;
+}
+RTP_DEV float sqrt_exact(float x) {  // sqrtf(x)
+  float s = sqrt_fast(x);
+  const bool slow = !fast_range(x) || x < 0.0f;
+  if (__ballot(slow)) {
+    asm volatile("");
+    if (slow) s = __builtin_sqrtf(x);
+  }
+  return s;
+}
+RTP_DEV float rsqrt_exact(float x) {  // 1 / sqrtf(x)  (vtkm::RMagnitude, CPU build)
+  float r = rcp_nr1(sqrt_fast(x));
+  const bool slow = !fast_range(x) || x < 0.0f;
+  if (__ballot(slow)) {
+    asm volatile("");
+    if (slow) r = 1.0f / __builtin_sqrtf(x);
+  }
+  return r;
+}
+// vtkm::RMagnitude on the CPU build: 1 / sqrt(x.x)
+RTP_DEV float rmag(f3 a) { return rsqrt_exact(dot(a, a)); }
+RTP_DEV float magn(f3 a) { return sqrt_exact(dot(a, a)); }
+RTP_DEV f3 unit_vector(f3 a) { return scl(a, rmag(a)); }  // vec3.h:38-42
 
 // ------------------------------------------------------------------ RNG ---
 // wangXor.h:30-38; the draw replaces the state (wangXor.h:55-59)
@@ -128,35 +192,90 @@ RTP_DEV f3 local(const Onb& o, f3 a) {  // onb.h:27-28
 // -------------------------------------------------------- intersection ---
 // Lagae-Dutre ray/quad (Surface.h:31-161) on precomputed edges; returns the
 // ray parameter through t_out.  The bilinear (u,v) are never read downstream.
-RTP_DEV bool quad_hit(const DevQuad& Q, f3 o, f3 d, float& t_out) {
+// Branch-free form: every rejection test of the reference is evaluated on the
+// same values and the hit is their conjunction (the early returns only skip
+// work, they never change a value that a later test reads).
+RTP_DEV bool quad_hit_general(const DevQuad& Q, f3 o, f3 d, float& t_out) {
   const f3 e03 = ld3(Q.e03), e01 = ld3(Q.e01);
   f3 P = cross(d, e03);
   float det = dot(e01, P);
-  if (fabsf(det) < kEps) return false;
-  float inv_det = 1.0f / det;
+  float inv_det = rcp_exact(det);
   f3 T = sub(o, ld3(Q.v00));
   float alpha = dot(T, P) * inv_det;
-  if (alpha < 0.0f) return false;
   f3 Qv = cross(T, e01);
   float beta = dot(d, Qv) * inv_det;
-  if (beta < 0.0f) return false;
-  if ((alpha + beta) > 1.0f) {
+  float t = dot(e03, Qv) * inv_det;
+  bool ok = !(fabsf(det) < kEps) && !(alpha < 0.0f) && !(beta < 0.0f) && !(t < 0.0f);
+  if (ok && (alpha + beta) > 1.0f) {
     const f3 e23 = ld3(Q.e23), e21 = ld3(Q.e21);
     f3 Pp = cross(d, e21);
     float detp = dot(e23, Pp);
-    if (fabsf(detp) < kEps) return false;
-    float inv_detp = 1.0f / detp;
+    float inv_detp = rcp_exact(detp);
     f3 Tp = sub(o, ld3(Q.v11));
     float ap = dot(Tp, Pp) * inv_detp;
-    if (ap < 0.0f) return false;
     f3 Qp = cross(Tp, e23);
     float bp = dot(d, Qp) * inv_detp;
-    if (bp < 0.0f) return false;
+    ok = !(fabsf(detp) < kEps) && !(ap < 0.0f) && !(bp < 0.0f);
   }
-  float t = dot(e03, Qv) * inv_det;
-  if (t < 0.0f) return false;
   t_out = t;
-  return true;
+  return ok;
+}
+
+// Axis-aligned rectangle: e01 = a*e_I, e03 = b*e_J, e21 = b2*e_J, e23 =
+// a2*e_I (classified on the host from exact zeros).  The reference's products
+// with the exactly-zero edge components are +-0, and x + (+-0) == x,
+// x - (+-0) == x, (+-0) - x == -x for x != 0; every zero-valued intermediate
+// only ever reaches a comparison or a product, so its sign is irrelevant.
+// Each nonzero intermediate is therefore bit-identical to the general form,
+// and two-term sums are order-free, so this computes the same hit and t.
+template <int I, int J>
+RTP_DEV bool quad_hit_aa(const DevQuad& Q, f3 o, f3 d, float& t_out) {
+  constexpr int J1 = (J + 1) % 3, J2 = (J + 2) % 3, I1 = (I + 1) % 3, I2 = (I + 2) % 3;
+  const float a = Q.a, b = Q.b;
+  const float dv[3] = {d.x, d.y, d.z};
+  const float Tv[3] = {o.x - Q.v00[0], o.y - Q.v00[1], o.z - Q.v00[2]};
+  float P[3] = {0.f, 0.f, 0.f};
+  P[J1] = dv[J2] * b;         // cross(d, b e_J)
+  P[J2] = -(dv[J1] * b);
+  const float det = a * P[I];  // dot(e01, P)
+  const float inv_det = rcp_exact(det);
+  const float alpha = (Tv[J1] * P[J1] + Tv[J2] * P[J2]) * inv_det;
+  float Qv[3] = {0.f, 0.f, 0.f};
+  Qv[I1] = Tv[I2] * a;        // cross(T, a e_I)
+  Qv[I2] = -(Tv[I1] * a);
+  const float beta = (dv[I1] * Qv[I1] + dv[I2] * Qv[I2]) * inv_det;
+  const float t = (b * Qv[J]) * inv_det;  // dot(e03, Q) * inv_det
+  bool ok = !(fabsf(det) < kEps) && !(alpha < 0.0f) && !(beta < 0.0f) && !(t < 0.0f);
+  if (ok && (alpha + beta) > 1.0f) {
+    const float a2 = Q.a2, b2 = Q.b2;
+    const float Tp[3] = {o.x - Q.v11[0], o.y - Q.v11[1], o.z - Q.v11[2]};
+    float Pp[3] = {0.f, 0.f, 0.f};
+    Pp[J1] = dv[J2] * b2;     // cross(d, b2 e_J)
+    Pp[J2] = -(dv[J1] * b2);
+    const float detp = a2 * Pp[I];
+    const float inv_detp = rcp_exact(detp);
+    const float ap = (Tp[J1] * Pp[J1] + Tp[J2] * Pp[J2]) * inv_detp;
+    float Qp[3] = {0.f, 0.f, 0.f};
+    Qp[I1] = Tp[I2] * a2;     // cross(Tp, a2 e_I)
+    Qp[I2] = -(Tp[I1] * a2);
+    const float bp = (dv[I1] * Qp[I1] + dv[I2] * Qp[I2]) * inv_detp;
+    ok = !(fabsf(detp) < kEps) && !(ap < 0.0f) && !(bp < 0.0f);
+  }
+  t_out = t;
+  return ok;
+}
+
+// Q.kind is wave-uniform (every lane tests the same quad): scalar branch.
+RTP_DEV bool quad_hit(const DevQuad& Q, f3 o, f3 d, float& t_out) {
+  switch (Q.kind) {
+    case 1: return quad_hit_aa<0, 1>(Q, o, d, t_out);
+    case 2: return quad_hit_aa<0, 2>(Q, o, d, t_out);
+    case 3: return quad_hit_aa<1, 0>(Q, o, d, t_out);
+    case 4: return quad_hit_aa<1, 2>(Q, o, d, t_out);
+    case 5: return quad_hit_aa<2, 0>(Q, o, d, t_out);
+    case 6: return quad_hit_aa<2, 1>(Q, o, d, t_out);
+    default: return quad_hit_general(Q, o, d, t_out);
+  }
 }
 
 // SphereLeafIntersector::hit (Surface.h:319-367): first acceptable root
@@ -167,7 +286,7 @@ RTP_DEV bool sphere_hit(f3 o, f3 d, float tmin, float tmax, f3 c, float rr, floa
   float cc = dot(oc, oc) - rr;
   float disc = b * b - a * cc;
   if (disc > 0) {
-    float sq = __builtin_sqrtf(b * b - a * cc);
+    float sq = sqrt_exact(b * b - a * cc);
     float temp = (-b - sq) / a;
     if (temp < tmax && temp > tmin) {
       t_out = temp;
@@ -184,17 +303,17 @@ RTP_DEV bool sphere_hit(f3 o, f3 d, float tmin, float tmax, f3 c, float rr, floa
 
 // ----------------------------------------------------------- sampling ---
 RTP_DEV f3 random_cosine_direction(float r1, float r2) {  // PdfWorklet.h:47-53
-  float z = __builtin_sqrtf(1 - r2);
+  float z = sqrt_exact(1 - r2);
   float phi = (float)(2 * kPi * r1);
-  float x = rtp_cosf(phi) * 2 * __builtin_sqrtf(r2);
-  float y = rtp_sinf(phi) * 2 * __builtin_sqrtf(r2);
+  float x = rtp_cosf(phi) * 2 * sqrt_exact(r2);
+  float y = rtp_sinf(phi) * 2 * sqrt_exact(r2);
   return mk(x, y, z);
 }
 RTP_DEV f3 random_to_sphere(float rr, float dist2, float r1, float r2) {  // PdfWorklet.h:157-165
-  float z = 1 + r2 * (__builtin_sqrtf(1 - rr / dist2) - 1);
+  float z = 1 + r2 * (sqrt_exact(1 - rr / dist2) - 1);
   float phi = (float)(2 * kPi * r1);
-  float x = rtp_cosf(phi) * __builtin_sqrtf(1 - z * z);
-  float y = rtp_sinf(phi) * __builtin_sqrtf(1 - z * z);
+  float x = rtp_cosf(phi) * sqrt_exact(1 - z * z);
+  float y = rtp_sinf(phi) * sqrt_exact(1 - z * z);
   return mk(x, y, z);
 }
 
@@ -215,9 +334,9 @@ RTP_DEV float sphere_pdf_value(const DevLights& L, f3 o, f3 v) {
   f3 c = ld3(L.sc);
   if (sphere_hit(o, v, 0.001f, 3.40282347e+38f, c, L.srr, t)) {
     f3 co = sub(c, o);
-    float cos_theta_max = __builtin_sqrtf(1 - L.srr / dot(co, co));
+    float cos_theta_max = sqrt_exact(1 - L.srr / dot(co, co));
     float solid_angle = (float)(2 * kPi * (1 - cos_theta_max));
-    return 1 / solid_angle;
+    return rcp_exact(solid_angle);  // 1 / solid_angle
   }
   return 0;
 }
@@ -248,7 +367,7 @@ RTP_DEV void dielectric_scatter(f3 dir, f3 n, float ref_idx, float rnd, f3& sd) 
     float dt = dot(uv, outward);
     float discriminant = (float)(1.0 - ni_over_nt * ni_over_nt * (1 - dt * dt));
     if (discriminant > 0) {
-      refracted = sub(scl(sub(uv, scl(outward, dt)), ni_over_nt), scl(outward, __builtin_sqrtf(discriminant)));
+      refracted = sub(scl(sub(uv, scl(outward, dt)), ni_over_nt), scl(outward, sqrt_exact(discriminant)));
       reflect_prob = schlick(cosine, ref_idx);
     } else {
       reflect_prob = 1.0f;

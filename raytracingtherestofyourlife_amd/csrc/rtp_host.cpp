@@ -8,7 +8,9 @@
 // is IEEE single/double, the same as the reference's g++ build).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -17,8 +19,12 @@
 #include "../../include/rtp.h"
 #include "rtp_layout.hpp"
 
-extern "C" hipError_t rtp_launch_render(const rtp::KParams* p, hipStream_t stream);
+extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int* variant_out, int* waves_out);
+extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::KParams* p, int variant, int waves,
+                                        hipStream_t stream);
 extern "C" hipError_t rtp_launch_eval_primitive(int kind, const void* in, void* out, int64_t n, hipStream_t stream);
+extern "C" hipError_t rtp_launch_verify_fast_math(int kind, uint32_t lo, uint64_t count, unsigned long long* bad,
+                                                  uint32_t* first_bad, hipStream_t stream);
 
 namespace {
 
@@ -79,6 +85,23 @@ void fill_quad(rtp::DevQuad& Q, v3 q, v3 r, v3 s, v3 t) {
   st(Q.e21, sub(r, s));
   st(Q.e23, sub(t, s));
   st(Q.n, normalize(cross(sub(r, q), sub(s, q))));  // TriangleNormal(q,r,s), Surface.h:182-183
+  // axis-aligned rectangle?  (exact zeros only; see quad_hit_aa)
+  auto axis_of = [](const float* e) -> int {
+    int nz = 0, ax = -1;
+    for (int k = 0; k < 3; k++)
+      if (e[k] != 0.0f) nz++, ax = k;
+    return nz == 1 ? ax : -1;
+  };
+  const int I = axis_of(Q.e01), J = axis_of(Q.e03);
+  Q.kind = 0;
+  if (I >= 0 && J >= 0 && I != J && axis_of(Q.e21) == J && axis_of(Q.e23) == I) {
+    static const int kinds[3][3] = {{0, 1, 2}, {3, 0, 4}, {5, 6, 0}};
+    Q.kind = kinds[I][J];
+    Q.a = Q.e01[I];
+    Q.b = Q.e03[J];
+    Q.a2 = Q.e23[I];
+    Q.b2 = Q.e21[J];
+  }
 }
 
 bool bit_equal(const float* a, const float* b, int n) { return std::memcmp(a, b, sizeof(float) * n) == 0; }
@@ -91,6 +114,8 @@ struct rtp_context {
   bool has_scene = false;
   float* d_hist = nullptr;
   size_t hist_bytes = 0;
+  unsigned long long* d_dbg = nullptr;  // RTP_DEBUG_STATS=1: per-wave counters of the last launch
+  int dbg_waves = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
@@ -125,6 +150,7 @@ void rtp_destroy(rtp_context* c) {
   hipSetDevice(c->device);
   if (c->d_scene) hipFree(c->d_scene);
   if (c->d_hist) hipFree(c->d_hist);
+  if (c->d_dbg) hipFree(c->d_dbg);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
   delete c;
@@ -151,6 +177,7 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
   rtp::DevScene* h = new rtp::DevScene();
   std::memset(h, 0, sizeof(*h));
   std::vector<int> kept;
+  std::vector<rtp::DevQuad> built;
   for (int q = 0; q < s->n_quads; q++) {
     const int32_t* id = s->quad_points + 4 * q;
     for (int k = 0; k < 4; k++)
@@ -177,12 +204,27 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
       delete h;
       return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_set_scene: too many distinct quads");
     }
-    rtp::DevQuad& Q = h->quads[kept.size()];
+    rtp::DevQuad Q;
     fill_quad(Q, ld(s->points + 3 * id[0]), ld(s->points + 3 * id[1]), ld(s->points + 3 * id[2]),
               ld(s->points + 3 * id[3]));
     Q.mt = s->mat_type[s->quad_mat[q]];
     st(Q.alb, ld(s->tex_rgb + 3 * s->tex_type[s->quad_tex[q]]));
+    Q.orig = (int32_t)kept.size();  // rank in the reference's (index) order
     kept.push_back(q);
+    built.push_back(Q);
+  }
+  // group by kind (1..6 axis-aligned, then 0 general); the device scan compares
+  // (t, orig) lexicographically, which is exactly the reference's index-order
+  // strict '<' scan, so the grouping changes no result.
+  {
+    const int order[7] = {1, 2, 3, 4, 5, 6, 0};
+    int pos = 0;
+    for (int g = 0; g < 7; g++) {
+      h->kind_begin[g] = pos;
+      for (const rtp::DevQuad& Q : built)
+        if (Q.kind == order[g]) h->quads[pos++] = Q;
+    }
+    h->kind_begin[7] = pos;
   }
   h->n_quads = (int32_t)kept.size();
   for (int k = 0; k < s->n_spheres; k++) {
@@ -289,7 +331,6 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
                   uint32_t* d_seed, uint32_t* d_live, hipStream_t stream, double* kernel_ms) {
   HIP_TRY(hipSetDevice(c->device));
   rtp::KParams p{};
-  p.scene = c->d_scene;
   camera_setup(cam, nx, ny, &p.cam);
   p.nx = nx, p.ny = ny, p.spp = spp, p.depth = depth;
   p.seed_base = seed_base;
@@ -299,12 +340,26 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
   p.out = d_out;
   p.seed_out = d_seed;
   p.live_out = d_live;
-  size_t hist_need = (size_t)(depth > 1 ? depth - 1 : 1) * (size_t)npix * 16;
+  int variant = 2, waves = 0;
+  const int64_t lanes = rtp_plan_history_lanes(npix, &variant, &waves);
+  size_t hist_need = (size_t)(depth > 1 ? depth - 1 : 1) * (size_t)lanes * 16;
   rtp_status rs = ensure_hist(c, hist_need);
   if (rs != RTP_OK) return rs;
   p.hist = c->d_hist;
+  p.dbg = nullptr;
+  {
+    const char* e = getenv("RTP_DEBUG_STATS");
+    if (e && e[0] == '1' && variant == 2) {
+      if (c->d_dbg) hipFree(c->d_dbg);
+      c->d_dbg = nullptr;
+      HIP_TRY(hipMalloc(&c->d_dbg, (size_t)waves * rtp::kDbgCounters * 8));
+      HIP_TRY(hipMemsetAsync(c->d_dbg, 0, (size_t)waves * rtp::kDbgCounters * 8, stream));
+      c->dbg_waves = waves;
+      p.dbg = c->d_dbg;
+    }
+  }
   if (kernel_ms) HIP_TRY(hipEventRecord(c->ev0, stream));
-  HIP_TRY(rtp_launch_render(&p, stream));
+  HIP_TRY(rtp_launch_render(c->d_scene, &p, variant, waves, stream));
   if (kernel_ms) {
     HIP_TRY(hipEventRecord(c->ev1, stream));
     HIP_TRY(hipEventSynchronize(c->ev1));
@@ -422,6 +477,26 @@ rtp_status rtp_render_device(rtp_context* c, const rtp_camera* cam, int32_t nx, 
   return rs;
 }
 
+// Diagnostics: sums of the pool kernel's per-wave counters from the last launch
+// made with RTP_DEBUG_STATS=1 (order of rtp::DbgCounter); returns the number
+// of waves, 0 if none were recorded.
+int32_t rtp_debug_counters(rtp_context* c, uint64_t* out, int32_t n_out) {
+  if (!c || !c->d_dbg || !out) return 0;
+  std::vector<unsigned long long> h((size_t)c->dbg_waves * rtp::kDbgCounters);
+  if (hipMemcpy(h.data(), c->d_dbg, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  for (int k = 0; k < n_out && k < rtp::kDbgCounters; k++) {
+    uint64_t acc = 0;
+    for (int w = 0; w < c->dbg_waves; w++) acc += h[(size_t)w * rtp::kDbgCounters + k];
+    out[k] = acc;
+  }
+  if (n_out > rtp::kDbgCounters) {  // extra slot: max wave lifetime
+    uint64_t mx = 0;
+    for (int w = 0; w < c->dbg_waves; w++) mx = std::max<uint64_t>(mx, h[(size_t)w * rtp::kDbgCounters + rtp::kDbgCyclesTotal]);
+    out[rtp::kDbgCounters] = mx;
+  }
+  return c->dbg_waves;
+}
+
 rtp_status rtp_eval_primitive(rtp_context* c, int32_t kind, const void* in, void* out, int64_t n) {
   if (!c || !in || !out || n < 0 || kind < 0 || kind > 3)
     return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_eval_primitive: bad arguments");
@@ -436,6 +511,35 @@ rtp_status rtp_eval_primitive(rtp_context* c, int32_t kind, const void* in, void
   hipFree(din);
   if (dout) hipFree(dout);
   if (e != hipSuccess) return hip_fail(e, "rtp_eval_primitive");
+  return RTP_OK;
+}
+
+// Diagnostics: exhaustive device check of a fast arithmetic sequence (kind,
+// see rtp_verify_fast_math_kernel) over float bit patterns [lo_bits, hi_bits].
+rtp_status rtp_verify_fast_math(rtp_context* c, int32_t kind, uint32_t lo_bits, uint32_t hi_bits,
+                                uint64_t* mismatches, uint32_t* first_bad) {
+  if (!c || !mismatches || hi_bits < lo_bits) return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_verify_fast_math: bad args");
+  HIP_TRY(hipSetDevice(c->device));
+  unsigned long long* d_bad = nullptr;
+  uint32_t* d_first = nullptr;
+  HIP_TRY(hipMalloc(&d_bad, 8));
+  HIP_TRY(hipMalloc(&d_first, 4));
+  HIP_TRY(hipMemset(d_bad, 0, 8));
+  HIP_TRY(hipMemset(d_first, 0xff, 4));
+  const uint64_t total = (uint64_t)hi_bits - lo_bits + 1;
+  const uint64_t chunk = 1ull << 30;
+  for (uint64_t off = 0; off < total; off += chunk) {
+    const uint64_t n = std::min<uint64_t>(chunk, total - off);
+    HIP_TRY(rtp_launch_verify_fast_math(kind, lo_bits + (uint32_t)off, n, d_bad, d_first, nullptr));
+  }
+  unsigned long long bad = 0;
+  uint32_t first = 0;
+  HIP_TRY(hipMemcpy(&bad, d_bad, 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&first, d_first, 4, hipMemcpyDeviceToHost));
+  hipFree(d_bad);
+  hipFree(d_first);
+  *mismatches = bad;
+  if (first_bad) *first_bad = first;
   return RTP_OK;
 }
 

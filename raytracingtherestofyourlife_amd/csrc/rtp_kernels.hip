@@ -1,37 +1,86 @@
 // rtp_kernels.hip -- CDNA4 (gfx950) kernels of the path-tracing hot path.
 //
-// rtp_render_pixels_kernel: one lane per pixel, the lane runs the pixel's
-// whole sample x depth loop (MapperPathTracer.cxx:278-354) with the fused
-// per-depth stage sequence of SURVEY.md 3.2.  Scene and light data are read
-// with wave-uniform (scalar) loads; the only per-lane memory traffic is the
-// attenuation history (needed for the reference's back-to-front radiance
-// product, MapperPathTracer.cxx:328-348), kept depth-major [d][pixel] exactly
-// like the reference's ChannelBuffers so a wave's stores are coalesced.
+// Both kernels run the fused per-depth stage sequence of SURVEY.md 3.2 (one
+// call of bounce() == one depth of MapperPathTracer.cxx:286-305 for one ray)
+// and differ only in how work is mapped to lanes:
+//
+//  v1  rtp_render_lockstep: one lane per pixel; the lane walks its pixel's
+//      samples and depths in order (MapperPathTracer.cxx:278-354).  Lanes of
+//      a wave stay on the same depth, so a wave executes a live bounce as long
+//      as ANY of its 64 paths is alive -- kept as the simple reference mapping.
+//
+//  v2  rtp_render_pool (default): persistent waves.  Each wave owns a pool of
+//      pixels in LDS (RNG state, colour sum, sample count).  A lane always
+//      carries a LIVE path: when its path ends, the lane banks the sample's
+//      contribution into the pixel's slot, queues the pixel for the RNG
+//      fast-forward of its remaining dead depths, and immediately starts the
+//      next sample of a READY pixel.  The fast-forwards (pure integer Wang
+//      hashing) run in full-wave batches when the READY queue
+//      runs dry.  Per-pixel sample order, draw order and summation order are
+//      exactly the reference's; only the interleaving across pixels changes.
+//
+// Scene and light data are wave-uniform and arrive through a const __restrict__
+// kernel argument, so the compiler reads them with scalar loads into SGPRs.
+// The only per-lane global memory traffic is the attenuation history needed
+// by the reference's back-to-front radiance product (MapperPathTracer.cxx:
+// 328-348), stored depth-major [d][lane] like the reference's ChannelBuffers.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
 
 #include "rtp_device.hpp"
 
 namespace rtp {
 
-// Closest hit over every quad (index order, strict '<') then every sphere
-// with tmax from the quads: the closest-hit semantics of
-// BVHTraverser.h:128-227 over Surface.h:208-254 / 376-409.
 struct Hit {
   float t;
   int kind;  // -1 none, 0 quad, 1 sphere
   int idx;
 };
 
-RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d) {
-  Hit h{3.40282347e+38f, -1, 0};
-  const float tmin = 0.001f;
-  const int nq = sc->n_quads;
-  for (int q = 0; q < nq; q++) {
+// Closest hit over every quad then every sphere with tmax from the quads: the
+// closest-hit semantics of BVHTraverser.h:128-227 over Surface.h:208-254 /
+// 376-409 with quads visited in index order and a strict '<'.  That scan
+// returns the lexicographic minimum of (t, index) over the hits, so the quads
+// can be visited grouped by kind (one tight loop per axis-aligned orientation)
+// as long as equal t is broken by the original index.
+template <int I, int J>
+RTP_DEV void scan_aa(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d, Hit& h, int& best) {
+  for (int q = b; q < e; q++) {
+    const DevQuad& Q = sc->quads[q];
     float t;
-    if (quad_hit(sc->quads[q], o, d, t) && t < h.t && t > tmin) {
+    const bool ok = quad_hit_aa<I, J>(Q, o, d, t);
+    const int orig = Q.orig;
+    if (ok && t > 0.001f && (t < h.t || (t == h.t && orig < best))) {
       h.t = t;
       h.kind = 0;
       h.idx = q;
+      best = orig;
+    }
+  }
+}
+
+RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d) {
+  Hit h{3.40282347e+38f, -1, 0};
+  int best = 0x7fffffff;
+  const float tmin = 0.001f;
+  scan_aa<0, 1>(sc, sc->kind_begin[0], sc->kind_begin[1], o, d, h, best);
+  scan_aa<0, 2>(sc, sc->kind_begin[1], sc->kind_begin[2], o, d, h, best);
+  scan_aa<1, 0>(sc, sc->kind_begin[2], sc->kind_begin[3], o, d, h, best);
+  scan_aa<1, 2>(sc, sc->kind_begin[3], sc->kind_begin[4], o, d, h, best);
+  scan_aa<2, 0>(sc, sc->kind_begin[4], sc->kind_begin[5], o, d, h, best);
+  scan_aa<2, 1>(sc, sc->kind_begin[5], sc->kind_begin[6], o, d, h, best);
+  for (int q = sc->kind_begin[6]; q < sc->kind_begin[7]; q++) {
+    const DevQuad& Q = sc->quads[q];
+    float t;
+    const bool ok = quad_hit_general(Q, o, d, t);
+    const int orig = Q.orig;
+    if (ok && t > tmin && (t < h.t || (t == h.t && orig < best))) {
+      h.t = t;
+      h.kind = 0;
+      h.idx = q;
+      best = orig;
     }
   }
   const int ns = sc->n_spheres;
@@ -47,173 +96,391 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d) {
   return h;
 }
 
-__global__ void __launch_bounds__(256) rtp_render_pixels_kernel(KParams p) {
+// Camera::RayGen (Camera.cxx:482-524): 2 draws, jittered direction
+RTP_DEV f3 camera_ray(const DevCamera& cam, int pi, int pj, int nx, int ny, uint32_t& seed) {
+  float ru = randf(seed);
+  float rv = randf(seed);
+  f3 rd = add(add(ld3(cam.nlook), scl(ld3(cam.dx), ((2.f * ((float)pi + (1.f - ru)) - (float)nx) / 2.0f))),
+              scl(ld3(cam.dy), ((2.f * ((float)pj + rv) - (float)ny) / 2.0f)));
+  if (rd.x == 0.f) rd.x += 0.0000001f;
+  if (rd.y == 0.f) rd.y += 0.0000001f;
+  if (rd.z == 0.f) rd.z += 0.0000001f;
+  float sq_mag = __builtin_sqrtf(dot(rd, rd));
+  return mk(rd.x / sq_mag, rd.y / sq_mag, rd.z / sq_mag);
+}
+
+struct Path {
+  f3 org, dir;
+  int d;           // current depth (the path is alive at the start of depth d)
+  bool nonfinite;  // some stored A[d'] (d' <= D-2) is +-Inf or NaN
+};
+
+enum BounceResult { kAlive = 0, kMissed = 1, kLight = 2 };
+
+// One depth for a ray that is alive at its start:
+// intersect, collect, material, generate, pdfs, scatter.  Advances the RNG by
+// exactly the reference's draws for this depth and stores A[d] at hist_d
+// (when d <= D-2).  On kLight, `emit` receives E[d].
+RTP_DEV unsigned long long stamp(bool on) { return on ? __builtin_amdgcn_s_memtime() : 0ull; }
+
+RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3& emit, float4* __restrict__ hist_d,
+                   int D, unsigned long long* dbg = nullptr) {
+  const bool st = dbg != nullptr;
+  const unsigned long long t0 = stamp(st);
+  const uint32_t t1 = sc->which_t1, t2 = sc->which_t2;
+  const DevLights& L = sc->light;
+  const f3 org = ps.org, dir = ps.dir;
+  const int d = ps.d;
+  // intersect + CollectIntersecttWorklet (SurfaceWorklets.h:104-109)
+  Hit h = closest_hit(sc, org, dir);
+  if (st) {
+    const unsigned long long t1s = __builtin_amdgcn_s_memtime();
+    dbg[kDbgCyclesIntersect] += t1s - t0;
+  }
+  if (h.kind < 0) {
+    seed = dead_step(seed, t1, t2);  // which + generator draws of the now-dead ray
+    return kMissed;
+  }
+  f3 hp = add(org, scl(dir, h.t));
+  f3 hn;
+  int mt;
+  f3 alb;
+  if (h.kind == 0) {
+    const DevQuad& Q = sc->quads[h.idx];
+    hn = ld3(Q.n);
+    if (dot(hn, dir) > 0.f) hn = neg(hn);  // Surface.h:184-185
+    mt = Q.mt;
+    alb = ld3(Q.alb);
+  } else {
+    const DevSphere& S = sc->spheres[h.idx];
+    hn = mk((hp.x - S.c[0]) / S.r, (hp.y - S.c[1]) / S.r, (hp.z - S.c[2]) / S.r);
+    mt = S.mt;
+    alb = ld3(S.alb);
+  }
+  // applyMaterials (EmitWorklet.h)
+  if (mt == 1) {  // DiffuseLightWorklet: emit, path ends (status &= 0)
+    emit = (dot(hn, dir) < 0.0f) ? alb : mk(0.f, 0.f, 0.f);
+    seed = dead_step(seed, t1, t2);
+    return kLight;
+  }
+  f3 atten;
+  if (mt == 2) {  // DielectricWorklet: 1 draw before generation, specular
+    float r = randf(seed);
+    f3 sd;
+    dielectric_scatter(dir, hn, sc->ior, r, sd);
+    seed = dead_step(seed, t1, t2);  // generation draws (direction unused)
+    (void)randf(seed);               // SpherePDFWorklet's discarded draw
+    atten = mk(1.f, 1.f, 1.f);
+    ps.org = hp;
+    ps.dir = sd;
+  } else {  // LambertianWorklet
+    f3 gen;
+    uint32_t tw = wang(seed);  // which (PdfWorklet.h:20)
+    seed = tw;
+    if (tw < t1) {  // cosine (PdfWorklet.h:63-79)
+      float r1 = randf(seed);
+      float r2 = randf(seed);
+      Onb uvw = build_from_w(hn);
+      gen = de_nan(local(uvw, random_cosine_direction(r1, r2)));
+    } else if (tw < t2) {  // light quad (PdfWorklet.h:112-137)
+      float r1 = randf(seed);
+      float r2 = randf(seed);
+      float r3 = randf(seed);
+      f3 rp = mk(L.gx0 + r1 * L.gdx, L.gy0 + r2 * L.gdy, L.gz0 + r3 * L.gdz);
+      gen = sub(rp, hp);
+    } else {  // light sphere (PdfWorklet.h:193-213); g++ evaluates the draws right to left
+      float first = randf(seed);
+      float second = randf(seed);
+      f3 direction = sub(ld3(L.sc), hp);
+      float dist2 = dot(direction, direction);
+      Onb uvw = build_from_w(direction);
+      gen = de_nan(local(uvw, random_to_sphere(L.srr, dist2, second, first)));
+    }
+    // applyPDFs: QuadPDFWorklet, SpherePDFWorklet (1 discarded draw)
+    const float weight = 0.5f;
+    float sum = 0;
+    sum += weight * quad_pdf_value(L, hp, gen);
+    (void)randf(seed);
+    sum += weight * sphere_pdf_value(L, hp, gen);
+    // PDFCosineWorklet (ScatterWorklet.h:96-112): mixture in double
+    Onb uvw = build_from_w(hn);
+    float cv;
+    {
+      float cosine = dot(unit_vector(gen), uvw.w);
+      cv = (cosine > 0) ? (float)(cosine / kPi) : 0.f;
+    }
+    double pdf_val = 0.5 * (double)sum + 0.5 * (double)cv;
+    float sp;
+    {
+      float cosine = dot(hn, unit_vector(gen));
+      sp = (cosine < 0) ? 0.f : (float)(cosine / kPi);
+    }
+    double sctr = (double)sp / pdf_val;
+    atten = mk((float)(alb.x * sctr), (float)(alb.y * sctr), (float)(alb.z * sctr));
+    ps.org = hp;
+    ps.dir = gen;
+  }
+  if (d <= D - 2) {
+    *hist_d = make_float4(atten.x, atten.y, atten.z, 0.f);
+    ps.nonfinite |= !(__builtin_isfinite(atten.x) && __builtin_isfinite(atten.y) && __builtin_isfinite(atten.z));
+  }
+  return kAlive;
+}
+
+// Back-to-front radiance (MapperPathTracer.cxx:328-348) of a finished path:
+// s = E[D-1]+0; s = A[d]*s; s = E[d]+s for d = D-2..0.  Depths after the end
+// contribute A=1, E=0 exactly, so for a light hit at depth k this is
+// s = E_k (+0), then s = 0 + A[d]*s for d = k-1..0; for any other ending it
+// is +0, or NaN if some stored A was not finite (Inf*0 / NaN propagation).
+RTP_DEV f3 path_radiance(int result, int k, f3 emit, bool nonfinite, const float4* __restrict__ hist,
+                         int64_t stride) {
+  if (result != kLight) {
+    const float v = nonfinite ? __builtin_nanf("") : 0.0f;
+    return mk(v, v, v);
+  }
+  float sx = emit.x + 0.0f, sy = emit.y + 0.0f, sz = emit.z + 0.0f;
+  for (int dd = k - 1; dd >= 0; dd--) {
+    float4 a = hist[(int64_t)dd * stride];
+    sx = a.x * sx;
+    sy = a.y * sy;
+    sz = a.z * sz;
+    sx = 0.0f + sx;
+    sy = 0.0f + sy;
+    sz = 0.0f + sz;
+  }
+  return mk(sx, sy, sz);
+}
+
+RTP_DEV int64_t pixel_of(const KParams& p, int64_t k) { return p.pixel_ids ? p.pixel_ids[k] : p.pixel_begin + k; }
+
+// ------------------------------------------------------------------ v1 ---
+__global__ void __launch_bounds__(256) rtp_render_lockstep(const DevScene* __restrict__ sc, KParams p) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= p.npix) return;
-  const DevScene* __restrict__ sc = p.scene;
-  const int64_t pix = p.pixel_ids ? p.pixel_ids[k] : p.pixel_begin + k;
+  const int64_t pix = pixel_of(p, k);
   const uint32_t t1 = sc->which_t1, t2 = sc->which_t2;
-  const float ior = sc->ior;
-  const DevLights& L = sc->light;
-
   uint32_t seed = p.seed_base + (uint32_t)pix;  // seeds[i] = i (MapperPathTracer.cxx:265-267)
   float cr = 0.f, cg = 0.f, cb = 0.f;
   uint32_t live = 0;
   const int pi = (int32_t)pix % p.nx, pj = (int32_t)pix / p.nx;
-  const f3 eye = ld3(p.cam.eye), nlook = ld3(p.cam.nlook), cdx = ld3(p.cam.dx), cdy = ld3(p.cam.dy);
   float4* __restrict__ hist = reinterpret_cast<float4*>(p.hist) + k;
-  const int64_t hstride = p.npix;
+  const int64_t stride = p.npix;
   const int D = p.depth;
-
   for (int s = 0; s < p.spp; s++) {
-    // Camera::RayGen (Camera.cxx:482-524)
-    f3 dir;
-    {
-      float ru = randf(seed);
-      float rv = randf(seed);
-      f3 rd = add(add(nlook, scl(cdx, ((2.f * ((float)pi + (1.f - ru)) - (float)p.nx) / 2.0f))),
-                  scl(cdy, ((2.f * ((float)pj + rv) - (float)p.ny) / 2.0f)));
-      if (rd.x == 0.f) rd.x += 0.0000001f;
-      if (rd.y == 0.f) rd.y += 0.0000001f;
-      if (rd.z == 0.f) rd.z += 0.0000001f;
-      float sq_mag = __builtin_sqrtf(dot(rd, rd));
-      dir = mk(rd.x / sq_mag, rd.y / sq_mag, rd.z / sq_mag);
-    }
-    f3 org = eye;
-    bool alive = true;
-    int klight = -1;
+    Path ps;
+    ps.dir = camera_ray(p.cam, pi, pj, p.nx, p.ny, seed);
+    ps.org = ld3(p.cam.eye);
+    ps.nonfinite = false;
+    int result = kAlive, k_end = D;
     f3 emit = mk(0.f, 0.f, 0.f);
-    bool nonfinite = false;
-
     for (int d = 0; d < D; d++) {
-      if (!alive) {
+      if (result != kAlive) {
         seed = dead_step(seed, t1, t2);
         continue;
       }
       live++;
-      // intersect + CollectIntersecttWorklet (SurfaceWorklets.h:104-109)
-      Hit h = closest_hit(sc, org, dir);
-      if (h.kind < 0) {
-        alive = false;
-        seed = dead_step(seed, t1, t2);
-        continue;
-      }
-      f3 hp = add(org, scl(dir, h.t));
-      f3 hn;
-      int mt;
-      f3 alb;
-      if (h.kind == 0) {
-        const DevQuad& Q = sc->quads[h.idx];
-        hn = ld3(Q.n);
-        if (dot(hn, dir) > 0.f) hn = neg(hn);  // Surface.h:184-185
-        mt = Q.mt;
-        alb = ld3(Q.alb);
-      } else {
-        const DevSphere& S = sc->spheres[h.idx];
-        hn = mk((hp.x - S.c[0]) / S.r, (hp.y - S.c[1]) / S.r, (hp.z - S.c[2]) / S.r);
-        mt = S.mt;
-        alb = ld3(S.alb);
-      }
-      // applyMaterials (EmitWorklet.h)
-      if (mt == 1) {  // DiffuseLightWorklet: emit, path ends (status &= 0)
-        emit = (dot(hn, dir) < 0.0f) ? alb : mk(0.f, 0.f, 0.f);
-        klight = d;
-        alive = false;
-        seed = dead_step(seed, t1, t2);  // the dead ray still draws which + generator
-        continue;
-      }
-      f3 atten;
-      if (mt == 2) {  // DielectricWorklet: 1 draw before generation, specular
-        float r = randf(seed);
-        f3 sd;
-        dielectric_scatter(dir, hn, ior, r, sd);
-        // generation + discarded sphere-pdf draw only advance the stream
-        seed = dead_step(seed, t1, t2);
-        (void)randf(seed);
-        atten = mk(1.f, 1.f, 1.f);
-        org = hp;
-        dir = sd;
-      } else {  // LambertianWorklet
-        // generateRays: which + generator (PdfWorklet.h:19-213)
-        f3 gen;
-        uint32_t tw = wang(seed);
-        seed = tw;
-        if (tw < t1) {  // cosine
-          float r1 = randf(seed);
-          float r2 = randf(seed);
-          Onb uvw = build_from_w(hn);
-          gen = de_nan(local(uvw, random_cosine_direction(r1, r2)));
-        } else if (tw < t2) {  // light quad
-          float r1 = randf(seed);
-          float r2 = randf(seed);
-          float r3 = randf(seed);
-          f3 rp = mk(L.gx0 + r1 * L.gdx, L.gy0 + r2 * L.gdy, L.gz0 + r3 * L.gdz);
-          gen = sub(rp, hp);
-        } else {  // light sphere; g++ evaluates the two draws right to left
-          float first = randf(seed);
-          float second = randf(seed);
-          f3 c = ld3(L.sc);
-          f3 direction = sub(c, hp);
-          float dist2 = dot(direction, direction);
-          Onb uvw = build_from_w(direction);
-          gen = de_nan(local(uvw, random_to_sphere(L.srr, dist2, second, first)));
-        }
-        // applyPDFs: QuadPDFWorklet, SpherePDFWorklet (1 discarded draw)
-        const float weight = 0.5f;
-        float sum = 0;
-        sum += weight * quad_pdf_value(L, hp, gen);
-        (void)randf(seed);
-        sum += weight * sphere_pdf_value(L, hp, gen);
-        // PDFCosineWorklet (ScatterWorklet.h:96-112), mixture in double
-        Onb uvw = build_from_w(hn);
-        float cv;
-        {
-          float cosine = dot(unit_vector(gen), uvw.w);
-          cv = (cosine > 0) ? (float)(cosine / kPi) : 0.f;
-        }
-        double pdf_val = 0.5 * (double)sum + 0.5 * (double)cv;
-        float sp;
-        {
-          float cosine = dot(hn, unit_vector(gen));
-          sp = (cosine < 0) ? 0.f : (float)(cosine / kPi);
-        }
-        double sctr = (double)sp / pdf_val;
-        atten = mk((float)(alb.x * sctr), (float)(alb.y * sctr), (float)(alb.z * sctr));
-        org = hp;
-        dir = gen;
-      }
-      if (d <= D - 2) {
-        hist[(int64_t)d * hstride] = make_float4(atten.x, atten.y, atten.z, 0.f);
-        nonfinite |= !(__builtin_isfinite(atten.x) && __builtin_isfinite(atten.y) && __builtin_isfinite(atten.z));
-      }
+      ps.d = d;
+      result = bounce(sc, ps, seed, emit, hist + (int64_t)d * stride, D);
+      if (result != kAlive) k_end = d;
     }
-    // backward radiance (MapperPathTracer.cxx:328-348): s = E[D-1]+0, then
-    // s = A[d]*s; s = E[d]+s.  Dead depths contribute A=1, E=0 exactly.
-    float sx, sy, sz;
-    if (klight >= 0) {
-      sx = emit.x + 0.0f;
-      sy = emit.y + 0.0f;
-      sz = emit.z + 0.0f;
-      for (int d = klight - 1; d >= 0; d--) {
-        float4 a = hist[(int64_t)d * hstride];
-        sx = a.x * sx;
-        sy = a.y * sy;
-        sz = a.z * sz;
-        sx = 0.0f + sx;
-        sy = 0.0f + sy;
-        sz = 0.0f + sz;
-      }
-    } else {
-      const float v = nonfinite ? __builtin_nanf("") : 0.0f;
-      sx = sy = sz = v;
-    }
-    cr = cr + sx;
-    cg = cg + sy;
-    cb = cb + sz;
+    f3 c = path_radiance(result, k_end, emit, ps.nonfinite, hist, stride);
+    cr = cr + c.x;
+    cg = cg + c.y;
+    cb = cb + c.z;
   }
   reinterpret_cast<float4*>(p.out)[k] = make_float4(cr, cg, cb, 0.f);
   if (p.seed_out) p.seed_out[k] = seed;
   if (p.live_out) p.live_out[k] = live;
+}
+
+// ------------------------------------------------------------------ v2 ---
+constexpr int kWavesPerBlock = 4;
+constexpr int kPool = 256;  // pixel slots per wave (power of two: queue index = cursor & (kPool-1))
+// LDS per wave: seed, r, g, b, samples, live (u32) + rem, q_ready, q_ff, pad (u16)
+constexpr int kSlotBytes = 6 * 4 + 4 * 2;
+constexpr int kPoolLdsBytes = kWavesPerBlock * kPool * kSlotBytes;
+
+RTP_DEV uint32_t lane_rank(uint64_t mask) {  // number of set mask bits below this lane
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+RTP_DEV void wave_sync() {  // order LDS traffic between lanes of this wave (no cross-wave barrier)
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+#ifndef RTP_POOL_MIN_WAVES_PER_EU
+#define RTP_POOL_MIN_WAVES_PER_EU 1
+#endif
+template <bool kStats>
+__global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_pool(const DevScene* __restrict__ sc, KParams p, int n_waves) {
+  __shared__ __align__(16) unsigned char smem[kPoolLdsBytes];
+  const int lane = threadIdx.x & 63;
+  const int wib = threadIdx.x >> 6;
+  const int w = blockIdx.x * kWavesPerBlock + wib;  // global wave id
+  if (w >= n_waves) return;                          // whole wave leaves; no block-level barriers are used
+  unsigned char* base = smem + (size_t)wib * kPool * kSlotBytes;
+  uint32_t* s_seed = reinterpret_cast<uint32_t*>(base);
+  float* s_r = reinterpret_cast<float*>(s_seed + kPool);
+  float* s_g = s_r + kPool;
+  float* s_b = s_g + kPool;
+  uint32_t* s_samples = reinterpret_cast<uint32_t*>(s_b + kPool);
+  uint32_t* s_live = s_samples + kPool;
+  uint16_t* s_rem = reinterpret_cast<uint16_t*>(s_live + kPool);
+  uint16_t* q_ready = s_rem + kPool;
+  uint16_t* q_ff = q_ready + kPool;
+
+  const uint32_t t1 = sc->which_t1, t2 = sc->which_t2;
+  const int D = p.depth, S = p.spp;
+  // slot j of wave w <-> list entry k = j * n_waves + w (pixels interleaved over waves)
+  const int64_t left = p.npix - w;
+  const int n_slots = left <= 0 ? 0 : (int)min<int64_t>(kPool, (left + n_waves - 1) / n_waves);
+  for (int j = lane; j < n_slots; j += 64) {
+    const int64_t k = (int64_t)j * n_waves + w;
+    s_seed[j] = p.seed_base + (uint32_t)pixel_of(p, k);  // seeds[i] = i (MapperPathTracer.cxx:265-267)
+    s_r[j] = 0.f;
+    s_g[j] = 0.f;
+    s_b[j] = 0.f;
+    s_samples[j] = 0u;
+    s_live[j] = 0u;
+    s_rem[j] = 0;
+    q_ready[j] = (uint16_t)j;
+  }
+  wave_sync();
+  // wave-uniform, monotone queue cursors
+  int ready_head = 0, ready_tail = (S > 0) ? n_slots : 0, ff_head = 0, ff_tail = 0;
+
+  float4* __restrict__ hist = reinterpret_cast<float4*>(p.hist) + ((int64_t)w * 64 + lane);
+  const int64_t stride = (int64_t)n_waves * 64;
+  const f3 eye = ld3(p.cam.eye);
+
+  // diagnostics (uniform branch on a kernel argument; off in production)
+  // (compiled in only for the kStats instantiation: the counters cost ~30 VGPRs)
+  unsigned long long dbg[kStats ? kDbgCounters : 1] = {};
+  constexpr bool want_dbg = kStats;
+  const unsigned long long t_start = want_dbg ? __builtin_amdgcn_s_memtime() : 0ull;
+
+  bool has_path = false;
+  int slot = 0;
+  uint32_t seed = 0;
+  Path ps;
+  ps.org = eye;
+  ps.dir = mk(0.f, 0.f, 1.f);
+  ps.d = 0;
+  ps.nonfinite = false;
+
+  for (;;) {
+    const uint64_t idle = __ballot(!has_path);
+    const int n_idle = __popcll(idle);
+    const int n_ready = ready_tail - ready_head;
+    const int n_ff = ff_tail - ff_head;
+    if (n_ready < n_idle && n_ff > 0) {
+      // ---- batch RNG fast-forward over the remaining dead depths of finished
+      //      samples (1 + {2,3,2} draws per depth) ----
+      const unsigned long long t0 = want_dbg ? __builtin_amdgcn_s_memtime() : 0ull;
+      const int n = min(64, n_ff);
+      const bool mine = lane < n;
+      int fslot = 0, frem = 0;
+      uint32_t fseed = 0;
+      if (mine) {
+        fslot = q_ff[(ff_head + lane) & (kPool - 1)];
+        fseed = s_seed[fslot];
+        frem = s_rem[fslot];
+      }
+      int iters = 0;
+      for (int i = 0;; i++) {
+        const bool act = mine && i < frem;
+        if (!__any(act)) break;
+        if (act) fseed = dead_step(fseed, t1, t2);
+        iters++;
+      }
+      bool again = false;
+      if (mine) {
+        s_seed[fslot] = fseed;
+        again = s_samples[fslot] < (uint32_t)S;
+      }
+      const uint64_t push = __ballot(again);
+      if (again) q_ready[(ready_tail + (int)lane_rank(push)) & (kPool - 1)] = (uint16_t)fslot;
+      ready_tail += __popcll(push);
+      ff_head += n;
+      wave_sync();
+      if (want_dbg) {
+        dbg[kDbgFfPhases] += 1;
+        dbg[kDbgFfLanes] += (unsigned long long)n;
+        dbg[kDbgFfIters] += (unsigned long long)iters;
+        dbg[kDbgCyclesFf] += __builtin_amdgcn_s_memtime() - t0;
+      }
+      continue;
+    }
+    // ---- refill idle lanes with the next sample of READY pixels ----
+    const unsigned long long tb = stamp(want_dbg);
+    const int take = min(n_idle, n_ready);
+    if (!has_path) {
+      const int r = (int)lane_rank(idle);
+      if (r < take) {
+        slot = q_ready[(ready_head + r) & (kPool - 1)];
+        seed = s_seed[slot];
+        const int64_t pix = pixel_of(p, (int64_t)slot * n_waves + w);
+        const int pi = (int32_t)pix % p.nx, pj = (int32_t)pix / p.nx;
+        ps.dir = camera_ray(p.cam, pi, pj, p.nx, p.ny, seed);
+        ps.org = eye;
+        ps.d = 0;
+        ps.nonfinite = false;
+        has_path = true;
+      }
+    }
+    ready_head += take;
+    if (!__any(has_path)) break;  // nothing live, nothing READY, nothing to fast-forward
+    if (want_dbg) dbg[kDbgCyclesRefill] += __builtin_amdgcn_s_memtime() - tb;
+    // ---- one depth of every live path ----
+    bool ended = false;
+    const unsigned long long ta = stamp(want_dbg);
+    unsigned long long tbnc = ta;
+    if (has_path) {
+      f3 emit = mk(0.f, 0.f, 0.f);
+      const int res = bounce(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D, want_dbg ? dbg : nullptr);
+      tbnc = stamp(want_dbg);
+      if (res == kAlive && ps.d < D - 1) {
+        ps.d++;
+      } else {
+        const int k_end = ps.d;
+        const f3 c = path_radiance(res, k_end, emit, ps.nonfinite, hist, stride);
+        s_r[slot] = s_r[slot] + c.x;  // cols += sumtotl (MapperPathTracer.cxx:350), in sample order
+        s_g[slot] = s_g[slot] + c.y;
+        s_b[slot] = s_b[slot] + c.z;
+        s_samples[slot] = s_samples[slot] + 1u;
+        s_live[slot] = s_live[slot] + (uint32_t)(k_end + 1);
+        s_seed[slot] = seed;
+        s_rem[slot] = (uint16_t)(D - 1 - k_end);
+        ended = true;
+        has_path = false;
+      }
+    }
+    if (want_dbg) {
+      const unsigned long long te = __builtin_amdgcn_s_memtime();
+      dbg[kDbgCyclesShade] += tbnc - ta;  // minus the intersect share, subtracted on the host
+      dbg[kDbgCyclesEnd] += te - tbnc;
+    }
+    const uint64_t fin = __ballot(ended);
+    if (ended) q_ff[(ff_tail + (int)lane_rank(fin)) & (kPool - 1)] = (uint16_t)slot;
+    ff_tail += __popcll(fin);
+    wave_sync();
+    if (want_dbg) {
+      dbg[kDbgBounceSteps] += 1;
+      dbg[kDbgBounceLanes] += (unsigned long long)__popcll(__ballot(has_path || ended));
+      dbg[kDbgCyclesBounce] += __builtin_amdgcn_s_memtime() - tb;
+    }
+  }
+  if (want_dbg && lane == 0) {
+    dbg[kDbgCyclesTotal] = __builtin_amdgcn_s_memtime() - t_start;
+    for (int c = 0; c < (kStats ? kDbgCounters : 0); c++) p.dbg[(int64_t)w * kDbgCounters + c] = dbg[c];
+  }
+  wave_sync();
+  for (int j = lane; j < n_slots; j += 64) {
+    const int64_t k = (int64_t)j * n_waves + w;
+    reinterpret_cast<float4*>(p.out)[k] = make_float4(s_r[j], s_g[j], s_b[j], 0.f);
+    if (p.seed_out) p.seed_out[k] = s_seed[j];
+    if (p.live_out) p.live_out[k] = s_live[j];
+  }
 }
 
 // ------------------------------------------------------- diagnostics ---
@@ -233,14 +500,89 @@ __global__ void rtp_eval_primitive_kernel(int kind, const void* in, void* out, i
   }
 }
 
+// Exhaustive equivalence check of a fast sequence against the IEEE operation
+// for every float bit pattern in [lo, hi] (one lane per pattern).
+__global__ void rtp_verify_fast_math_kernel(int kind, uint32_t lo, uint64_t count, unsigned long long* bad,
+                                            uint32_t* first_bad) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const uint32_t bits = lo + (uint32_t)i;
+  const float x = __uint_as_float(bits);
+  float want = 0.f, got = 0.f;
+  switch (kind) {
+    case 0: want = 1.0f / x; got = rcp_nr1(x); break;
+    case 1: want = 1.0f / x; got = rcp_nr2(x); break;
+    case 2: want = __builtin_sqrtf(x); got = sqrt_fast(x); break;
+    case 3: want = 1.0f / __builtin_sqrtf(x); got = rcp_nr1(sqrt_fast(x)); break;
+    case 4: want = 1.0f / __builtin_sqrtf(x); got = rcp_nr2(sqrt_fast(x)); break;
+    default: break;
+  }
+  if (__float_as_uint(want) != __float_as_uint(got)) {
+    atomicAdd(bad, 1ull);
+    atomicMin(first_bad, bits);
+  }
+}
+
 }  // namespace rtp
 
 // ----------------------------------------------------------- launchers ---
-extern "C" hipError_t rtp_launch_render(const rtp::KParams* p, hipStream_t stream) {
+extern "C" hipError_t rtp_launch_verify_fast_math(int kind, uint32_t lo, uint64_t count, unsigned long long* bad,
+                                                  uint32_t* first_bad, hipStream_t stream) {
   const int block = 256;
-  const int64_t grid = (p->npix + block - 1) / block;
-  if (grid <= 0) return hipSuccess;
-  hipLaunchKernelGGL(rtp::rtp_render_pixels_kernel, dim3((unsigned)grid), dim3(block), 0, stream, *p);
+  const uint64_t grid = (count + block - 1) / block;
+  if (grid == 0) return hipSuccess;
+  hipLaunchKernelGGL(rtp::rtp_verify_fast_math_kernel, dim3((unsigned)grid), dim3(block), 0, stream, kind, lo, count,
+                     bad, first_bad);
+  return hipGetLastError();
+}
+namespace {
+int pool_resident_waves() {
+  static int cached = -1;
+  if (cached > 0) return cached;
+  int dev = 0, cus = 0, nb = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 1024;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtp::rtp_render_pool<false>, 256, 0) != hipSuccess || nb <= 0) nb = 1;
+  cached = cus * nb * rtp::kWavesPerBlock;
+  return cached;
+}
+int kernel_variant() {
+  const char* e = getenv("RTP_KERNEL");
+  if (e && e[0] == '1') return 1;
+  return 2;
+}
+}  // namespace
+
+// Work plan: how many lanes' worth of attenuation history the launch needs.
+extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int* variant_out, int* waves_out) {
+  const int v = kernel_variant();
+  if (variant_out) *variant_out = v;
+  if (v == 1) {
+    if (waves_out) *waves_out = (int)((npix + 63) / 64);
+    return npix;
+  }
+  const int64_t by_lanes = (npix + 63) / 64;
+  const int64_t by_pool = (npix + rtp::kPool - 1) / rtp::kPool;
+  int64_t W = std::min<int64_t>(by_lanes, pool_resident_waves());
+  W = std::max<int64_t>(W, by_pool);
+  W = std::max<int64_t>(W, 1);
+  if (waves_out) *waves_out = (int)W;
+  return W * 64;
+}
+
+extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::KParams* p, int variant, int waves,
+                                        hipStream_t stream) {
+  if (p->npix <= 0) return hipSuccess;
+  if (variant == 1) {
+    const int64_t grid = (p->npix + 255) / 256;
+    hipLaunchKernelGGL(rtp::rtp_render_lockstep, dim3((unsigned)grid), dim3(256), 0, stream, scene, *p);
+  } else {
+    const int blocks = (waves + rtp::kWavesPerBlock - 1) / rtp::kWavesPerBlock;
+    if (p->dbg)
+      hipLaunchKernelGGL(rtp::rtp_render_pool<true>, dim3((unsigned)blocks), dim3(256), 0, stream, scene, *p, waves);
+    else
+      hipLaunchKernelGGL(rtp::rtp_render_pool<false>, dim3((unsigned)blocks), dim3(256), 0, stream, scene, *p, waves);
+  }
   return hipGetLastError();
 }
 

@@ -14,14 +14,19 @@ constexpr int kMaxQuads = 256;
 constexpr int kMaxSpheres = 256;
 
 // One quad of the Lagae-Dutre test (Surface.h:31-161) with v00=q, v10=r,
-// v11=s, v01=t.  128 B, read with uniform (scalar) loads.
+// v11=s, v01=t.  Read with uniform (scalar) loads.
 struct alignas(16) DevQuad {
   float v00[3], e01[3], e03[3];  // e01 = v10-v00, e03 = v01-v00
   float v11[3], e21[3], e23[3];  // e21 = v10-v11, e23 = v01-v11
   float n[3];                    // Normalize(TriangleNormal(q,r,s)), unflipped
   float alb[3];                  // tex[texType[texIdx]]
   int32_t mt;                    // matType[matIdx]
-  int32_t pad[7];
+  // kind 0: general; 1..6: axis-aligned rectangle with e01 = a*e_I, e03 =
+  // b*e_J, e21 = b2*e_J, e23 = a2*e_I, (I,J) = (0,1),(0,2),(1,0),(1,2),(2,0),(2,1)
+  int32_t kind;
+  float a, b, a2, b2;
+  int32_t orig;  // index in the reference's quad order (tie-break of equal t)
+  int32_t pad;
 };
 
 struct alignas(16) DevSphere {
@@ -47,6 +52,9 @@ struct alignas(16) DevLights {
 struct alignas(16) DevScene {
   int32_t n_quads;
   int32_t n_spheres;
+  // quads are stored grouped by kind: kind k occupies [kind_begin[k], kind_begin[k+1])
+  // in the order k = 1..6, then 0 (kind_begin[7] == n_quads for the general group's end)
+  int32_t kind_begin[8];
   uint32_t which_t1;  // smallest hash with which >= 2   (PdfWorklet.h:20)
   uint32_t which_t2;  // smallest hash with which == 3
   float ior;
@@ -62,7 +70,6 @@ struct DevCamera {
 };
 
 struct KParams {
-  const DevScene* scene;
   DevCamera cam;
   int32_t nx, ny, spp, depth;
   uint32_t seed_base;
@@ -72,7 +79,25 @@ struct KParams {
   float* out;                // float4[npix]
   uint32_t* seed_out;        // nullable
   uint32_t* live_out;        // nullable
-  float* hist;               // float4[(depth-1) * npix] attenuation history
+  float* hist;               // float4[(depth-1) * lanes] attenuation history, depth-major
+  unsigned long long* dbg;   // nullable: per-wave counters (kDbgCounters each), diagnostics only
+};
+
+// per-wave diagnostic counters of the pool kernel (RTP_DEBUG_STATS=1)
+enum DbgCounter {
+  kDbgBounceSteps = 0,   // loop iterations that ran a bounce
+  kDbgBounceLanes,       // sum over those iterations of lanes with a live path
+  kDbgFfPhases,          // fast-forward batches
+  kDbgFfLanes,           // sum of batch sizes
+  kDbgFfIters,           // sum of per-batch loop trip counts (max remaining depths)
+  kDbgCyclesBounce,      // s_memtime cycles spent in bounce steps (incl. refill)
+  kDbgCyclesFf,          // s_memtime cycles spent in fast-forward batches
+  kDbgCyclesTotal,       // whole wave lifetime
+  kDbgCyclesIntersect,   // inside bounce(): closest_hit
+  kDbgCyclesShade,       // inside bounce(): material + generate + pdfs + scatter
+  kDbgCyclesEnd,         // path end: radiance product + slot update + queue push
+  kDbgCyclesRefill,      // refill: READY pop + camera ray
+  kDbgCounters
 };
 
 }  // namespace rtp

@@ -277,6 +277,29 @@ class Device:
                                         ctypes.byref(st) if timed else None))
         return st
 
+    DEBUG_COUNTERS = ("bounce_steps", "bounce_lanes", "ff_phases", "ff_lanes", "ff_iters", "cycles_bounce",
+                      "cycles_ff", "cycles_total", "cycles_intersect", "cycles_bounce_call", "cycles_end",
+                      "cycles_refill", "max_wave_cycles")
+
+    def debug_counters(self) -> dict:
+        """Pool-kernel counters of the last launch made with RTP_DEBUG_STATS=1."""
+        n = len(self.DEBUG_COUNTERS)
+        out = (ctypes.c_uint64 * n)()
+        waves = self._L.rtp_debug_counters(self.handle, out, n)
+        d = {k: int(v) for k, v in zip(self.DEBUG_COUNTERS, out)}
+        d["waves"] = int(waves)
+        return d
+
+    def verify_fast_math(self, kind: int, lo: float, hi: float) -> tuple[int, int]:
+        """Exhaustive device check over every float in [lo, hi] (same sign)."""
+        lb = int(np.float32(lo).view(np.uint32))
+        hb = int(np.float32(hi).view(np.uint32))
+        lb, hb = min(lb, hb), max(lb, hb)
+        bad = ctypes.c_uint64(0)
+        first = ctypes.c_uint32(0)
+        check(self._L.rtp_verify_fast_math(self.handle, kind, lb, hb, ctypes.byref(bad), ctypes.byref(first)))
+        return int(bad.value), int(first.value)
+
     def eval_primitive(self, kind: int, values: np.ndarray) -> np.ndarray:
         a = np.ascontiguousarray(values)
         assert a.dtype.itemsize == 4

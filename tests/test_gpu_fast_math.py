@@ -1,0 +1,25 @@
+"""The short reciprocal / sqrt sequences the kernels use in place of the IEEE
+lowering are bit-identical to it for EVERY float of the range they are used
+on (exhaustive, on the device).  Outside [2^-40, 2^40] the kernels fall back
+to the IEEE operation (rcp_exact / sqrt_exact / rsqrt_exact)."""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+LO, HI = 2.0**-40, 2.0**40
+
+
+@pytest.mark.parametrize("kind,name", [(0, "rcp"), (2, "sqrt"), (3, "rsqrt")])
+def test_fast_sequence_exact_on_whole_range(device, kind, name):
+    bad, first = device.verify_fast_math(kind, LO, HI)
+    assert bad == 0, f"{name}: {bad} mismatches, first bit pattern {first:#x}"
+    if kind == 0:
+        bad, first = device.verify_fast_math(kind, -LO, -HI)
+        assert bad == 0, f"{name} (negative): {bad} mismatches, first {first:#x}"
+
+
+def test_fast_range_boundaries_are_covered(device):
+    """The checked range includes every value the guards let through."""
+    import numpy as np
+
+    assert np.float32(LO) == np.float32(2.0**-40) and np.float32(HI) == np.float32(2.0**40)

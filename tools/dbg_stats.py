@@ -1,0 +1,34 @@
+"""Print the pool kernel's per-wave diagnostic counters for one render."""
+import argparse, json, os, sys
+os.environ["RTP_DEBUG_STATS"] = "1"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+import raytracingtherestofyourlife_amd as rtp
+ap = argparse.ArgumentParser()
+ap.add_argument("--spp", type=int, default=100)
+ap.add_argument("--depth", type=int, default=50)
+ap.add_argument("--n", type=int, default=800)
+ap.add_argument("--variant", type=int, default=0)
+a = ap.parse_args()
+dev = rtp.Device(0); dev.set_cornell_box(a.variant)
+out = torch.zeros((a.n * a.n, 4), dtype=torch.float32, device="cuda")
+live = torch.zeros(a.n * a.n, dtype=torch.int32, device="cuda")
+st = dev.render_device(rtp.default_camera(), a.n, a.n, a.spp, a.depth, out.data_ptr(),
+                       stream=torch.cuda.current_stream().cuda_stream, live_ptr=live.data_ptr(), timed=True)
+c = dev.debug_counters()
+samples = a.n * a.n * a.spp
+L = live.to(torch.int64).sum().item()
+c.update(kernel_ms=st.kernel_ms, samples=samples, live_bounces=L,
+         lanes_per_bounce_step=c["bounce_lanes"] / max(1, c["bounce_steps"]),
+         lanes_per_ff=c["ff_lanes"] / max(1, c["ff_phases"]),
+         ff_iters_per_phase=c["ff_iters"] / max(1, c["ff_phases"]),
+         frac_cycles_ff=c["cycles_ff"] / max(1, c["cycles_total"]),
+         frac_cycles_bounce=c["cycles_bounce"] / max(1, c["cycles_total"]),
+         cycles_per_bounce_step=c["cycles_bounce"] / max(1, c["bounce_steps"]),
+         cycles_per_ff_phase=c["cycles_ff"] / max(1, c["ff_phases"]),
+         avg_wave_over_max=c["cycles_total"] / max(1, c["waves"]) / max(1, c["max_wave_cycles"]),
+         per_step_intersect=c["cycles_intersect"] / max(1, c["bounce_steps"]),
+         per_step_shade=(c["cycles_bounce_call"] - c["cycles_intersect"]) / max(1, c["bounce_steps"]),
+         per_step_end=c["cycles_end"] / max(1, c["bounce_steps"]),
+         per_step_refill=c["cycles_refill"] / max(1, c["bounce_steps"]))
+print(json.dumps(c, indent=1))
