@@ -149,8 +149,9 @@ rtp_status rtp_eval_primitive(rtp_context* ctx, int32_t kind, const void* in, vo
 /* Diagnostics: with RTP_DEBUG_STATS=1 in the environment the render kernel
  * records per-wave counters (bounce steps, live lanes, fast-forward batches,
  * shader-clock cycles per phase); this sums them over waves into out[0..n_out)
- * (out[8], if requested, = the longest wave lifetime) and returns the wave
- * count of the last such launch (0 if none). */
+ * (out[kDbgCounters], if requested, = the longest wave lifetime) and returns
+ * the wave count of the last such launch (0 if none).  n_out < 0: copy the raw
+ * per-wave records (waves * kDbgCounters values) instead. */
 int32_t rtp_debug_counters(rtp_context* ctx, uint64_t* out, int32_t n_out);
 
 /* Diagnostics: exhaustively compare a fast device arithmetic sequence with the

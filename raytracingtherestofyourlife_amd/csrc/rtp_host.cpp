@@ -116,6 +116,7 @@ struct rtp_context {
   size_t hist_bytes = 0;
   unsigned long long* d_dbg = nullptr;  // RTP_DEBUG_STATS=1: per-wave counters of the last launch
   int dbg_waves = 0;
+  unsigned long long* d_progress = nullptr;  // global finished-sample counter of the pool kernel
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
@@ -139,6 +140,12 @@ rtp_status rtp_create(int32_t device, rtp_context** out) {
     delete c;
     return hip_fail(e, "hipMalloc(scene)");
   }
+  e = hipMalloc(&c->d_progress, 8);
+  if (e != hipSuccess) {
+    hipFree(c->d_scene);
+    delete c;
+    return hip_fail(e, "hipMalloc(progress)");
+  }
   HIP_TRY(hipEventCreate(&c->ev0));
   HIP_TRY(hipEventCreate(&c->ev1));
   *out = c;
@@ -151,6 +158,7 @@ void rtp_destroy(rtp_context* c) {
   if (c->d_scene) hipFree(c->d_scene);
   if (c->d_hist) hipFree(c->d_hist);
   if (c->d_dbg) hipFree(c->d_dbg);
+  if (c->d_progress) hipFree(c->d_progress);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
   delete c;
@@ -347,9 +355,11 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
   if (rs != RTP_OK) return rs;
   p.hist = c->d_hist;
   p.dbg = nullptr;
+  p.progress = c->d_progress;
+  HIP_TRY(hipMemsetAsync(c->d_progress, 0, 8, stream));
   {
     const char* e = getenv("RTP_DEBUG_STATS");
-    if (e && e[0] == '1' && variant == 2) {
+    if (e && (e[0] == '1' || e[0] == '2') && variant == 2) {  // 2: timestamps in the production kernel
       if (c->d_dbg) hipFree(c->d_dbg);
       c->d_dbg = nullptr;
       HIP_TRY(hipMalloc(&c->d_dbg, (size_t)waves * rtp::kDbgCounters * 8));
@@ -484,6 +494,10 @@ int32_t rtp_debug_counters(rtp_context* c, uint64_t* out, int32_t n_out) {
   if (!c || !c->d_dbg || !out) return 0;
   std::vector<unsigned long long> h((size_t)c->dbg_waves * rtp::kDbgCounters);
   if (hipMemcpy(h.data(), c->d_dbg, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  if (n_out < 0) {  // raw per-wave records: out must hold waves * kDbgCounters values
+    std::memcpy(out, h.data(), h.size() * 8);
+    return c->dbg_waves;
+  }
   for (int k = 0; k < n_out && k < rtp::kDbgCounters; k++) {
     uint64_t acc = 0;
     for (int w = 0; w < c->dbg_waves; w++) acc += h[(size_t)w * rtp::kDbgCounters + k];

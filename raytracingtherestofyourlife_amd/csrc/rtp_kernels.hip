@@ -308,8 +308,29 @@ RTP_DEV void wave_sync() {  // order LDS traffic between lanes of this wave (no 
   __builtin_amdgcn_wave_barrier();
 }
 
+// Issue-priority balancing: the SIMD arbiter favours older waves, so with a
+// static split of pixels the youngest wave of each SIMD finished ~1/3 later
+// than the oldest, and the SIMD ran its last milliseconds with one or two
+// waves (little latency hiding).  Every kPrioPeriod finished samples a wave publishes
+// its finished samples to a global counter and sets s_setprio from how far
+// its own completed fraction lags the global one.
+#ifndef RTP_PRIO_BALANCE
+#define RTP_PRIO_BALANCE 1
+#endif
+#ifndef RTP_PRIO_THR
+#define RTP_PRIO_THR 0.0002f
+#endif
+constexpr int kPrioPeriod = 128;
+
+RTP_DEV void set_priority(float lag) {  // s_setprio needs an immediate
+  if (lag > RTP_PRIO_THR) __builtin_amdgcn_s_setprio(3);
+  else if (lag > 0.0f) __builtin_amdgcn_s_setprio(2);
+  else if (lag > -RTP_PRIO_THR) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+}
+
 #ifndef RTP_POOL_MIN_WAVES_PER_EU
-#define RTP_POOL_MIN_WAVES_PER_EU 1
+#define RTP_POOL_MIN_WAVES_PER_EU 4
 #endif
 template <bool kStats>
 __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_pool(const DevScene* __restrict__ sc, KParams p, int n_waves) {
@@ -358,6 +379,13 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
   unsigned long long dbg[kStats ? kDbgCounters : 1] = {};
   constexpr bool want_dbg = kStats;
   const unsigned long long t_start = want_dbg ? __builtin_amdgcn_s_memtime() : 0ull;
+  if (p.dbg && lane == 0) {  // placement + start time (RTP_DEBUG_STATS=1|2)
+    p.dbg[(int64_t)w * kDbgCounters + kDbgRealStart] = __builtin_amdgcn_s_memrealtime();
+    p.dbg[(int64_t)w * kDbgCounters + kDbgHwId] =
+        (unsigned)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));  // HW_REG_HW_ID
+  }
+
+  int published = 0;  // wave-uniform: finished samples already added to p.progress
 
   bool has_path = false;
   int slot = 0;
@@ -464,15 +492,28 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
     if (ended) q_ff[(ff_tail + (int)lane_rank(fin)) & (kPool - 1)] = (uint16_t)slot;
     ff_tail += __popcll(fin);
     wave_sync();
+    if (RTP_PRIO_BALANCE && ff_tail - published >= kPrioPeriod) {
+      // ff_tail counts this wave's finished samples
+      unsigned long long g = 0;
+      if (lane == 0) g = atomicAdd(p.progress, (unsigned long long)(ff_tail - published));
+      g = __shfl(g, 0) + (unsigned long long)(ff_tail - published);
+      published = ff_tail;
+      // completed fractions: global g / (npix*S) vs own ff_tail / (n_slots*S)
+      set_priority(((float)g / (float)p.npix - (float)ff_tail / (float)n_slots) / (float)S);
+    }
     if (want_dbg) {
       dbg[kDbgBounceSteps] += 1;
       dbg[kDbgBounceLanes] += (unsigned long long)__popcll(__ballot(has_path || ended));
       dbg[kDbgCyclesBounce] += __builtin_amdgcn_s_memtime() - tb;
     }
   }
+  if (!kStats && p.dbg && lane == 0)  // RTP_DEBUG_STATS=2: lifetime only
+    p.dbg[(int64_t)w * kDbgCounters + kDbgRealEnd] = __builtin_amdgcn_s_memrealtime();
   if (want_dbg && lane == 0) {
     dbg[kDbgCyclesTotal] = __builtin_amdgcn_s_memtime() - t_start;
-    for (int c = 0; c < (kStats ? kDbgCounters : 0); c++) p.dbg[(int64_t)w * kDbgCounters + c] = dbg[c];
+    dbg[kDbgRealEnd] = __builtin_amdgcn_s_memrealtime();
+    for (int c = 0; c < (kStats ? kDbgCounters : 0); c++)
+      if (c != kDbgRealStart && c != kDbgHwId) p.dbg[(int64_t)w * kDbgCounters + c] = dbg[c];
   }
   wave_sync();
   for (int j = lane; j < n_slots; j += 64) {
@@ -536,15 +577,17 @@ extern "C" hipError_t rtp_launch_verify_fast_math(int kind, uint32_t lo, uint64_
   return hipGetLastError();
 }
 namespace {
-int pool_resident_waves() {
-  static int cached = -1;
-  if (cached > 0) return cached;
+int pool_resident_waves(bool stats) {
+  static int cached[2] = {-1, -1};
+  if (cached[stats] > 0) return cached[stats];
   int dev = 0, cus = 0, nb = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 1024;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtp::rtp_render_pool<false>, 256, 0) != hipSuccess || nb <= 0) nb = 1;
-  cached = cus * nb * rtp::kWavesPerBlock;
-  return cached;
+  hipError_t e = stats ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtp::rtp_render_pool<true>, 256, 0)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtp::rtp_render_pool<false>, 256, 0);
+  if (e != hipSuccess || nb <= 0) nb = 1;
+  cached[stats] = cus * nb * rtp::kWavesPerBlock;
+  return cached[stats];
 }
 int kernel_variant() {
   const char* e = getenv("RTP_KERNEL");
@@ -563,7 +606,8 @@ extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int* variant_out, int* w
   }
   const int64_t by_lanes = (npix + 63) / 64;
   const int64_t by_pool = (npix + rtp::kPool - 1) / rtp::kPool;
-  int64_t W = std::min<int64_t>(by_lanes, pool_resident_waves());
+  const char* st = getenv("RTP_DEBUG_STATS");
+  int64_t W = std::min<int64_t>(by_lanes, pool_resident_waves(st && st[0] == '1'));
   W = std::max<int64_t>(W, by_pool);
   W = std::max<int64_t>(W, 1);
   if (waves_out) *waves_out = (int)W;
@@ -578,7 +622,8 @@ extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::K
     hipLaunchKernelGGL(rtp::rtp_render_lockstep, dim3((unsigned)grid), dim3(256), 0, stream, scene, *p);
   } else {
     const int blocks = (waves + rtp::kWavesPerBlock - 1) / rtp::kWavesPerBlock;
-    if (p->dbg)
+    const char* st = getenv("RTP_DEBUG_STATS");
+    if (p->dbg && st && st[0] == '1')
       hipLaunchKernelGGL(rtp::rtp_render_pool<true>, dim3((unsigned)blocks), dim3(256), 0, stream, scene, *p, waves);
     else
       hipLaunchKernelGGL(rtp::rtp_render_pool<false>, dim3((unsigned)blocks), dim3(256), 0, stream, scene, *p, waves);

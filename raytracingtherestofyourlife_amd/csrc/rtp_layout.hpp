@@ -81,6 +81,7 @@ struct KParams {
   uint32_t* live_out;        // nullable
   float* hist;               // float4[(depth-1) * lanes] attenuation history, depth-major
   unsigned long long* dbg;   // nullable: per-wave counters (kDbgCounters each), diagnostics only
+  unsigned long long* progress;  // zeroed before launch: samples finished by all waves (issue-priority balancing)
 };
 
 // per-wave diagnostic counters of the pool kernel (RTP_DEBUG_STATS=1)
@@ -97,6 +98,9 @@ enum DbgCounter {
   kDbgCyclesShade,       // inside bounce(): material + generate + pdfs + scatter
   kDbgCyclesEnd,         // path end: radiance product + slot update + queue push
   kDbgCyclesRefill,      // refill: READY pop + camera ray
+  kDbgRealStart,         // s_memrealtime (100 MHz, chip-wide) at wave start (raw, not summed)
+  kDbgRealEnd,           // ... at wave end
+  kDbgHwId,              // HW_REG_HW_ID of the wave (SIMD/CU/SE placement)
   kDbgCounters
 };
 

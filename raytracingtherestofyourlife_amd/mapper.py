@@ -279,7 +279,7 @@ class Device:
 
     DEBUG_COUNTERS = ("bounce_steps", "bounce_lanes", "ff_phases", "ff_lanes", "ff_iters", "cycles_bounce",
                       "cycles_ff", "cycles_total", "cycles_intersect", "cycles_bounce_call", "cycles_end",
-                      "cycles_refill", "max_wave_cycles")
+                      "cycles_refill", "real_start", "real_end", "hw_id", "max_wave_cycles")
 
     def debug_counters(self) -> dict:
         """Pool-kernel counters of the last launch made with RTP_DEBUG_STATS=1."""
@@ -299,6 +299,14 @@ class Device:
         first = ctypes.c_uint32(0)
         check(self._L.rtp_verify_fast_math(self.handle, kind, lb, hb, ctypes.byref(bad), ctypes.byref(first)))
         return int(bad.value), int(first.value)
+
+    def debug_wave_records(self) -> np.ndarray:
+        """Raw per-wave counter records [waves, kDbgCounters] of the last stats launch."""
+        n = len(self.DEBUG_COUNTERS) - 1
+        waves = self.debug_counters()["waves"]
+        buf = np.zeros((max(waves, 1), n), dtype=np.uint64)
+        self._L.rtp_debug_counters(self.handle, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), -1)
+        return buf[:waves]
 
     def eval_primitive(self, kind: int, values: np.ndarray) -> np.ndarray:
         a = np.ascontiguousarray(values)

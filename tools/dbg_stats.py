@@ -32,3 +32,16 @@ c.update(kernel_ms=st.kernel_ms, samples=samples, live_bounces=L,
          per_step_end=c["cycles_end"] / max(1, c["bounce_steps"]),
          per_step_refill=c["cycles_refill"] / max(1, c["bounce_steps"]))
 print(json.dumps(c, indent=1))
+rec = dev.debug_wave_records()
+import numpy as np
+start, end = rec[:, 12].astype(np.int64), rec[:, 13].astype(np.int64)
+t0 = start.min()
+life = (end - start) / 100.0  # us (100 MHz)
+fin = (end - t0) / 100.0
+print("wave start spread us", (start.max() - t0) / 100.0, "finish us: min/p10/p50/p90/max",
+      [round(float(np.percentile(fin, q)), 1) for q in (0, 10, 50, 90, 100)])
+hw = rec[:, 14].astype(np.int64)
+wave_id = hw & 0xF; simd = (hw >> 4) & 3; cu = (hw >> 8) & 0xF
+print("lifetime by wave-in-SIMD slot:", {int(s): round(float(life[wave_id == s].mean()), 1) for s in np.unique(wave_id)})
+order = np.argsort(start)
+print("lifetime of earliest-started quartile vs latest:", round(float(life[order[:len(order)//4]].mean()),1), round(float(life[order[-len(order)//4:]].mean()),1))
