@@ -54,5 +54,31 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+ROOT = os.path.dirname(HERE)
+# C++ host programs over the C ABI (include/rtp/rendering.hpp), linked with g++
+CPP_PROGRAMS = {
+    os.path.join(ROOT, "examples", "rtp_path"): os.path.join(ROOT, "examples", "path_main.cpp"),
+    os.path.join(ROOT, "tests", "cpp", "shim_check"): os.path.join(ROOT, "tests", "cpp", "shim_check.cpp"),
+}
+
+
+def build_cpp(force: bool = False) -> list[str]:
+    """g++ the C++ host programs against librtp.so (rpath to the package dir)."""
+    lib = build()
+    built = []
+    hdrs = [os.path.join(ROOT, "include", "rtp.h"), os.path.join(ROOT, "include", "rtp", "rendering.hpp"), lib]
+    for exe, src in CPP_PROGRAMS.items():
+        rel = os.path.relpath(HERE, os.path.dirname(exe))
+        if force or not os.path.exists(exe) or any(os.path.getmtime(d) > os.path.getmtime(exe) for d in hdrs + [src]):
+            cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-Wall", "-I", os.path.join(ROOT, "include"), src,
+                   "-L", HERE, "-lrtp", f"-Wl,-rpath,$ORIGIN/{rel}", "-o", exe]
+            res = subprocess.run(cmd, capture_output=True, text=True)
+            if res.returncode != 0:
+                raise RuntimeError(f"g++ failed for {src}:\n{res.stderr}")
+        built.append(exe)
+    return built
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print("\n".join(build_cpp(force="--force" in sys.argv)))
