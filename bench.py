@@ -49,9 +49,11 @@ def tile_pixels(nx: int, ny: int, rank: int, world: int) -> np.ndarray:
     return (rows * nx + cols).reshape(-1)
 
 
-def cpu_baseline(budget_s: float, nx: int, ny: int, depth: int) -> dict:
-    """Oracle stage-structured SoA pass sequence (the reference's cost model),
-    1 thread, spp=1, on a band of image rows sized to ~budget_s."""
+def cpu_baseline(budget_s: float, nx: int, ny: int, depth: int, nthreads: int = 1) -> dict:
+    """Oracle stage-structured SoA pass sequence (the reference's cost model:
+    every stage over every ray, no compaction), on the C2 camera: a band of
+    rows at 1 spp sized to ~budget_s, widened to the full frame and then to
+    more samples per pixel when one frame is cheaper than the budget."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_ctypes as oc
 
@@ -61,23 +63,34 @@ def cpu_baseline(budget_s: float, nx: int, ny: int, depth: int) -> dict:
     mid = ny // 2
     rows = 8
     t = time.perf_counter()
-    oc.render_soa(sc, cam, nx, ny, 1, depth, row_begin=mid - rows // 2, row_end=mid + rows // 2, nthreads=1)
+    oc.render_soa(sc, cam, nx, ny, 1, depth, row_begin=mid - rows // 2, row_end=mid + rows // 2, nthreads=nthreads)
     probe = time.perf_counter() - t
-    rows = int(max(8, min(ny, rows * budget_s / max(probe, 1e-3))))
+    want_rows = rows * budget_s / max(probe, 1e-3)
+    spp = max(1, int(want_rows / ny)) if want_rows > ny else 1
+    rows = int(max(8, min(ny, want_rows)))
     r0 = max(0, mid - rows // 2)
     r1 = min(ny, r0 + rows)
     t = time.perf_counter()
-    oc.render_soa(sc, cam, nx, ny, 1, depth, row_begin=r0, row_end=r1, nthreads=1)
+    oc.render_soa(sc, cam, nx, ny, spp, depth, row_begin=r0, row_end=r1, nthreads=nthreads)
     dt = time.perf_counter() - t
-    samples = (r1 - r0) * nx
+    samples = (r1 - r0) * nx * spp
     return {
         "value": samples / dt / 1e6,
         "unit": "Msamples/s",
-        "cores": 1,
+        "cores": nthreads,
         "kind": "port",
-        "sample": f"C2 camera {nx}x{ny}, rows {r0}-{r1} ({samples} pixels), 1 spp, depth {depth}, "
-                  f"stage-structured SoA oracle (cost/sample independent of spp), {dt:.1f}s",
+        "sample": f"C2 scene+camera {nx}x{ny}, rows {r0}-{r1} ({(r1 - r0) * nx} pixels) x {spp} spp, depth {depth}: "
+                  f"{samples} samples in {dt:.1f}s, stage-structured SoA oracle, {nthreads} thread(s)",
     }
+
+
+def host_threads() -> int:
+    """CPU share of this process (affinity), capped at 16 (the GPU box's share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
 
 
 def load_traffic(path: str, cfg: dict):
@@ -102,6 +115,7 @@ def main() -> None:
     ap.add_argument("--spp", type=int, default=1000)
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work (0: skip)")
+    ap.add_argument("--cpu-budget-mt", type=float, default=6.0, help="seconds of all-cores CPU baseline (0: skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c2.json"))
     args = ap.parse_args()
 
@@ -188,9 +202,11 @@ def main() -> None:
     traffic = load_traffic(args.traffic_json, cfg)
 
     if rank == 0:
-        cpu = None
+        cpu = cpu_mt = None
         if world == 1 and args.cpu_budget > 0:
             cpu = cpu_baseline(args.cpu_budget, args.nx, args.ny, args.depth)
+        if world == 1 and args.cpu_budget_mt > 0:
+            cpu_mt = cpu_baseline(args.cpu_budget_mt, args.nx, args.ny, args.depth, nthreads=host_threads())
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -222,6 +238,7 @@ def main() -> None:
                 "bytes_per_sample_model": round(bytes_per_sample, 3),
             },
             "cpu_baseline": cpu,
+            "cpu_baseline_all_cores": cpu_mt,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

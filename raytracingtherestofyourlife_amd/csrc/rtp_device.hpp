@@ -101,6 +101,25 @@ RTP_DEV float rsqrt_exact(float x) {  // 1 / sqrtf(x)  (vtkm::RMagnitude, CPU bu
   }
   return r;
 }
+// 1/det of the quad tests.  The reciprocal is only used when !(|det| < kEps)
+// (kEps = 1e-5 > 2^-40), so the small end of fast_range never matters: only
+// |det| > 2^40 (or NaN) takes the IEEE path.
+#ifndef RTP_RCP_DET_FAST
+#define RTP_RCP_DET_FAST 1
+#endif
+RTP_DEV float rcp_det(float x) {
+#if RTP_RCP_DET_FAST
+  float r = rcp_nr1(x);
+  const bool slow = !(fabsf(x) <= 0x1p40f);
+  if (__ballot(slow)) {
+    asm volatile("");
+    if (slow) r = 1.0f / x;
+  }
+  return r;
+#else
+  return rcp_exact(x);
+#endif
+}
 // vtkm::RMagnitude on the CPU build: 1 / sqrt(x.x)
 RTP_DEV float rmag(f3 a) { return rsqrt_exact(dot(a, a)); }
 RTP_DEV float magn(f3 a) { return sqrt_exact(dot(a, a)); }
@@ -173,6 +192,40 @@ RTP_DEV float glibc_sincosf(float y, int is_cos) {
 RTP_DEV float rtp_sinf(float y) { return glibc_sincosf(y, 0); }
 RTP_DEV float rtp_cosf(float y) { return glibc_sincosf(y, 1); }
 
+// sinf and cosf of the same argument, branch-free, each bit-identical to the
+// functions above (|y| < 120).  For |y| < pi/4 glibc's small-argument path is
+// the general path with n = 0 (x - 0*hpi == x, sign[0] == 1, table 0), so one
+// reduction serves every lane; both polynomials are evaluated and n's parity
+// says which is the sine.  Table 1 differs from table 0 only by negated cosine
+// coefficients, and negation commutes with round-to-nearest, so the even
+// polynomial of table 1 is exactly the negated one of table 0.
+RTP_DEV void rtp_sincosf(float y, float* sin_out, float* cos_out) {
+  const SinCosT& p = kSC[0];
+  const double x0 = y;
+  const double r = x0 * p.hpi_inv;
+  const int n = ((int32_t)r + 0x800000) >> 24;
+  const double x = x0 - n * p.hpi;
+  const double xs = ((n + 1) & 2) ? -x : x;  // sign[n & 3] = {1,-1,-1,1}
+  const double x2 = x * x;
+  // odd polynomial on xs (sinf_poly, n even branch)
+  const double x3 = xs * x2;
+  const double s1 = p.s2 + x2 * p.s3;
+  const double x7 = x3 * x2;
+  const float odd = (float)((xs + x3 * p.s1) + x7 * s1);
+  // even polynomial, table 0 (sinf_poly, n odd branch)
+  const double x4 = x2 * x2;
+  const double c2 = p.c3 + x2 * p.c4;
+  const double c1 = p.c0 + x2 * p.c1;
+  const double x6 = x4 * x2;
+  float even = (float)((c1 + x4 * p.c2) + x6 * c2);
+  even = (n & 2) ? -even : even;
+  float sv = (n & 1) ? even : odd;
+  float cv = (n & 1) ? odd : even;
+  const bool tiny = top12(y) < top12(0x1p-12f);
+  *sin_out = tiny ? y : sv;
+  *cos_out = tiny ? 1.0f : cv;
+}
+
 // ------------------------------------------------------------------ onb ---
 struct Onb {
   f3 u, v, w;
@@ -199,7 +252,7 @@ RTP_DEV bool quad_hit_general(const DevQuad& Q, f3 o, f3 d, float& t_out) {
   const f3 e03 = ld3(Q.e03), e01 = ld3(Q.e01);
   f3 P = cross(d, e03);
   float det = dot(e01, P);
-  float inv_det = rcp_exact(det);
+  float inv_det = rcp_det(det);
   f3 T = sub(o, ld3(Q.v00));
   float alpha = dot(T, P) * inv_det;
   f3 Qv = cross(T, e01);
@@ -210,7 +263,7 @@ RTP_DEV bool quad_hit_general(const DevQuad& Q, f3 o, f3 d, float& t_out) {
     const f3 e23 = ld3(Q.e23), e21 = ld3(Q.e21);
     f3 Pp = cross(d, e21);
     float detp = dot(e23, Pp);
-    float inv_detp = rcp_exact(detp);
+    float inv_detp = rcp_det(detp);
     f3 Tp = sub(o, ld3(Q.v11));
     float ap = dot(Tp, Pp) * inv_detp;
     f3 Qp = cross(Tp, e23);
@@ -238,7 +291,7 @@ RTP_DEV bool quad_hit_aa(const DevQuad& Q, f3 o, f3 d, float& t_out) {
   P[J1] = dv[J2] * b;         // cross(d, b e_J)
   P[J2] = -(dv[J1] * b);
   const float det = a * P[I];  // dot(e01, P)
-  const float inv_det = rcp_exact(det);
+  const float inv_det = rcp_det(det);
   const float alpha = (Tv[J1] * P[J1] + Tv[J2] * P[J2]) * inv_det;
   float Qv[3] = {0.f, 0.f, 0.f};
   Qv[I1] = Tv[I2] * a;        // cross(T, a e_I)
@@ -253,7 +306,7 @@ RTP_DEV bool quad_hit_aa(const DevQuad& Q, f3 o, f3 d, float& t_out) {
     Pp[J1] = dv[J2] * b2;     // cross(d, b2 e_J)
     Pp[J2] = -(dv[J1] * b2);
     const float detp = a2 * Pp[I];
-    const float inv_detp = rcp_exact(detp);
+    const float inv_detp = rcp_det(detp);
     const float ap = (Tp[J1] * Pp[J1] + Tp[J2] * Pp[J2]) * inv_detp;
     float Qp[3] = {0.f, 0.f, 0.f};
     Qp[I1] = Tp[I2] * a2;     // cross(Tp, a2 e_I)
@@ -299,6 +352,16 @@ RTP_DEV bool sphere_hit(f3 o, f3 d, float tmin, float tmax, f3 c, float rr, floa
     }
   }
   return false;
+}
+
+// (float)(cosine / kPi) of cosine_pdf::value (ScatterWorklet.h:96-112) as a
+// double product with the double reciprocal.  The two double results differ
+// by at most one double ulp; tests/test_gpu_fast_math.py checks exhaustively
+// (verify kind 5) that the float roundings agree for every float in [0, 2]
+// (the argument is a dot of two unit vectors, used only when > 0).
+RTP_DEV float cos_over_pi(float c) {
+  constexpr double kInvPi = 1.0 / kPi;
+  return (float)((double)c * kInvPi);
 }
 
 // ----------------------------------------------------------- sampling ---

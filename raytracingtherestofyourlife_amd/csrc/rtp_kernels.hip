@@ -31,6 +31,10 @@
 
 #include "rtp_device.hpp"
 
+#ifndef RTP_MERGED_GEN
+#define RTP_MERGED_GEN 1  // branch-free generator pass (bounce); 0: the three divergent branches
+#endif
+
 namespace rtp {
 
 struct Hit {
@@ -177,6 +181,38 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
     f3 gen;
     uint32_t tw = wang(seed);  // which (PdfWorklet.h:20)
     seed = tw;
+#if RTP_MERGED_GEN
+    // The three generators as one branch-free pass.  Cosine (PdfWorklet.h:
+    // 63-79) and light-sphere (:193-213) directions share the ONB, the
+    // sincos of phi = 2*pi*r1 and local(); they differ in w, in which draw
+    // is r1 (g++ evaluates the sphere generator's draws right to left), and
+    // in z and the radial factor.  The light-quad point (:112-137) needs a
+    // third draw, taken only by its lanes.
+    const bool is_cos = tw < t1, is_quad = !is_cos && tw < t2;
+    const float ra = randf(seed);
+    const float rb = randf(seed);
+    uint32_t s3 = seed;
+    const float rc = randf(s3);
+    seed = is_quad ? s3 : seed;
+    const f3 rp = mk(L.gx0 + ra * L.gdx, L.gy0 + rb * L.gdy, L.gz0 + rc * L.gdz);
+    const f3 genq = sub(rp, hp);
+    const f3 direction = sub(ld3(L.sc), hp);
+    const float r1 = is_cos ? ra : rb, r2 = is_cos ? rb : ra;
+    const f3 wdir = is_cos ? hn : direction;
+    const Onb guvw = build_from_w(wdir);
+    const float phi = (float)(2 * kPi * r1);
+    float sphi, cphi;
+    rtp_sincosf(phi, &sphi, &cphi);
+    // cosine: z = sqrt(1-r2), x = (cos(phi)*2)*sqrt(r2); sphere: z = 1 + r2*(sqrt(1-R^2/d^2)-1),
+    // x = cos(phi)*sqrt(1-z*z) (and (c*1)*s == c*s exactly)
+    const float dist2 = dot(direction, direction);
+    const float q = sqrt_exact(is_cos ? 1 - r2 : 1 - L.srr / dist2);
+    const float z = is_cos ? q : 1 + r2 * (q - 1);
+    const float rad = sqrt_exact(is_cos ? r2 : 1 - z * z);
+    const float m = is_cos ? 2.0f : 1.0f;
+    const f3 gcs = de_nan(local(guvw, mk(cphi * m * rad, sphi * m * rad, z)));
+    gen = is_quad ? genq : gcs;
+#else
     if (tw < t1) {  // cosine (PdfWorklet.h:63-79)
       float r1 = randf(seed);
       float r2 = randf(seed);
@@ -196,6 +232,7 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
       Onb uvw = build_from_w(direction);
       gen = de_nan(local(uvw, random_to_sphere(L.srr, dist2, second, first)));
     }
+#endif
     // applyPDFs: QuadPDFWorklet, SpherePDFWorklet (1 discarded draw)
     const float weight = 0.5f;
     float sum = 0;
@@ -207,13 +244,13 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
     float cv;
     {
       float cosine = dot(unit_vector(gen), uvw.w);
-      cv = (cosine > 0) ? (float)(cosine / kPi) : 0.f;
+      cv = (cosine > 0) ? cos_over_pi(cosine) : 0.f;
     }
     double pdf_val = 0.5 * (double)sum + 0.5 * (double)cv;
     float sp;
     {
       float cosine = dot(hn, unit_vector(gen));
-      sp = (cosine < 0) ? 0.f : (float)(cosine / kPi);
+      sp = (cosine < 0) ? 0.f : cos_over_pi(cosine);
     }
     double sctr = (double)sp / pdf_val;
     atten = mk((float)(alb.x * sctr), (float)(alb.y * sctr), (float)(alb.z * sctr));
@@ -370,7 +407,7 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
   // wave-uniform, monotone queue cursors
   int ready_head = 0, ready_tail = (S > 0) ? n_slots : 0, ff_head = 0, ff_tail = 0;
 
-  float4* __restrict__ hist = reinterpret_cast<float4*>(p.hist) + ((int64_t)w * 64 + lane);
+  float4* __restrict__ hist = reinterpret_cast<float4*>(p.hist) + ((int64_t)w * 64 + lane);  // [d][lane]
   const int64_t stride = (int64_t)n_waves * 64;
   const f3 eye = ld3(p.cam.eye);
 
@@ -556,6 +593,7 @@ __global__ void rtp_verify_fast_math_kernel(int kind, uint32_t lo, uint64_t coun
     case 2: want = __builtin_sqrtf(x); got = sqrt_fast(x); break;
     case 3: want = 1.0f / __builtin_sqrtf(x); got = rcp_nr1(sqrt_fast(x)); break;
     case 4: want = 1.0f / __builtin_sqrtf(x); got = rcp_nr2(sqrt_fast(x)); break;
+    case 5: want = (float)((double)x / kPi); got = cos_over_pi(x); break;
     default: break;
   }
   if (__float_as_uint(want) != __float_as_uint(got)) {

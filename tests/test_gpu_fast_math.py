@@ -23,3 +23,9 @@ def test_fast_range_boundaries_are_covered(device):
     import numpy as np
 
     assert np.float32(LO) == np.float32(2.0**-40) and np.float32(HI) == np.float32(2.0**40)
+
+
+def test_cos_over_pi_product_exact(device):
+    """(float)((double)c * (1/pi)) == (float)((double)c / pi) for every float c in [0, 2]."""
+    bad, first = device.verify_fast_math(5, 0.0, 2.0)
+    assert bad == 0, f"cos_over_pi: {bad} mismatches, first bit pattern {first:#x}"
