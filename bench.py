@@ -35,20 +35,6 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 TILE = 16
 
 
-def tile_pixels(nx: int, ny: int, rank: int, world: int) -> np.ndarray:
-    """Pixel ids of the 16x16 tiles owned by `rank` (tile t -> rank t % world),
-    each tile in row-major order (a 64-lane wave covers a 16x4 block)."""
-    tx, ty = nx // TILE, ny // TILE
-    assert tx * TILE == nx and ty * TILE == ny, "canvas must be a multiple of the tile size"
-    tiles = np.arange(tx * ty)
-    mine = tiles[tiles % world == rank]
-    oy, ox = np.divmod(mine, tx)
-    ly, lx = np.divmod(np.arange(TILE * TILE), TILE)
-    rows = (oy[:, None] * TILE + ly[None, :]).astype(np.int64)
-    cols = (ox[:, None] * TILE + lx[None, :]).astype(np.int64)
-    return (rows * nx + cols).reshape(-1)
-
-
 def cpu_baseline(budget_s: float, nx: int, ny: int, depth: int, nthreads: int = 1) -> dict:
     """Oracle stage-structured SoA pass sequence (the reference's cost model:
     every stage over every ray, no compaction), on the C2 camera: a band of
@@ -123,6 +109,7 @@ def main() -> None:
     import torch.distributed as dist
 
     import raytracingtherestofyourlife_amd as rtp
+    from raytracingtherestofyourlife_amd import shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -134,7 +121,7 @@ def main() -> None:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     nx, ny = args.nx, args.ny * world
-    ids_np = tile_pixels(nx, ny, rank, world)
+    ids_np = shard.tile_pixels(nx, ny, rank, world)
     npix = ids_np.size
     dev = rtp.Device(local)
     dev.set_cornell_box(0)

@@ -7,8 +7,10 @@
  * by tests/ (as the parity checker), by __graft_entry__.smoke() (checker) and
  * by bench.py's cpu_baseline leg (timed CPU baseline, kind "port").
  *
- * Parity status: the reference cannot be compiled here (needs VTK-m, absent,
- * see SURVEY.md 8c), so this restatement is pinned by (i) known-answer tests
+ * Parity status: PARITY UNPINNED against the reference itself.  The reference
+ * cannot be compiled here (needs VTK-m, absent) and holds no
+ * tests, golden images or fixtures for this path, so this restatement is only
+ * partially pinned, by (i) known-answer tests
  * probed on this host (RNG, glibc sinf/cosf bit-exactness, g++ argument
  * evaluation order) and (ii) the two internal variants (scalar per-pixel and
  * stage-structured SoA) agreeing bit-for-bit.  VTK-m behaviour that the

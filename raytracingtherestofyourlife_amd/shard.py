@@ -1,0 +1,105 @@
+"""Multi-GPU decomposition of the render, one process per GPU.
+
+Pixels are independent (own seed = pixel index, own sequential S x D stream,
+MapperPathTracer.cxx:265-267), so the path shards with no data exchange until
+the framebuffer sum:
+
+* image tiles (C2/C4): 16x16 tiles, tile t -> rank t mod G (static,
+  interleaved so every rank gets the same mix of cheap and expensive image
+  regions).  Each rank renders its pixel list into a zeroed canvas; ONE
+  reduce(sum) of the float4 canvas to rank 0.  Bit-exact: x + 0 == x and
+  NaN / Inf pass through the sum unchanged.
+* sample batches (C5): rank k renders S_k samples of every pixel with
+  seed = pixel + k*N (seed_base = k*N), then the same reduce.  A Wang-hash
+  stream has no jump-ahead and a pixel's sample-s state depends on every
+  earlier sample's variable draw count, so this is a documented derived
+  stream, exact against the oracle run on the same schedule.
+
+The render itself is a callback so the planner and the reduce are testable
+on CPU (gloo) with the oracle standing in for the device.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable
+
+import numpy as np
+
+TILE = 16
+
+
+def tile_pixels(nx: int, ny: int, rank: int, world: int, tile: int = TILE) -> np.ndarray:
+    """Pixel ids (int64, j*nx + i) of the tiles owned by `rank`; each tile in
+    row-major order, so a 64-lane wave covers a 16x4 block."""
+    if nx % tile or ny % tile:
+        raise ValueError(f"canvas {nx}x{ny} is not a multiple of the {tile}-pixel tile")
+    if not 0 <= rank < world:
+        raise ValueError("rank out of range")
+    tx, ty = nx // tile, ny // tile
+    tiles = np.arange(tx * ty)
+    mine = tiles[tiles % world == rank]
+    oy, ox = np.divmod(mine, tx)
+    ly, lx = np.divmod(np.arange(tile * tile), tile)
+    rows = (oy[:, None] * tile + ly[None, :]).astype(np.int64)
+    cols = (ox[:, None] * tile + lx[None, :]).astype(np.int64)
+    return (rows * nx + cols).reshape(-1)
+
+
+@dataclass(frozen=True)
+class SampleBatch:
+    rank: int
+    spp: int        # samples this rank renders per pixel
+    seed_base: int  # seed = pixel + seed_base (mod 2^32)
+
+
+def sample_batches(spp: int, world: int, npix: int) -> list[SampleBatch]:
+    """Split spp over `world` ranks (the first spp % world ranks take one more)."""
+    if spp < world:
+        raise ValueError("fewer samples than ranks")
+    base, extra = divmod(spp, world)
+    return [SampleBatch(k, base + (1 if k < extra else 0), (k * npix) & 0xFFFFFFFF) for k in range(world)]
+
+
+# render callbacks: (pixel_ids or None for all, spp, seed_base) -> float32 [n, 4] RGBA sums
+RenderFn = Callable[[np.ndarray | None, int, int], "np.ndarray"]
+
+
+def render_tile_shard(render: RenderFn, canvas, nx: int, ny: int, spp: int, rank: int, world: int):
+    """This rank's tiles into `canvas` (float32 [nx*ny, 4], numpy or torch),
+    zero elsewhere.  Returns the canvas."""
+    ids = tile_pixels(nx, ny, rank, world)
+    part = render(ids, spp, 0)
+    canvas[...] = 0
+    _scatter(canvas, ids, part)
+    return canvas
+
+
+def render_sample_shard(render: RenderFn, canvas, npix: int, spp: int, rank: int, world: int):
+    """This rank's sample batch of every pixel into `canvas`."""
+    b = sample_batches(spp, world, npix)[rank]
+    canvas[...] = _as_like(canvas, render(None, b.spp, b.seed_base))
+    return canvas
+
+
+def reduce_canvas(canvas, dist) -> None:
+    """The one collective: sum the float4 canvases onto rank 0."""
+    if dist.get_world_size() > 1:
+        dist.reduce(canvas, dst=0, op=dist.ReduceOp.SUM)
+
+
+def _as_like(canvas, a):
+    if isinstance(canvas, np.ndarray):
+        return np.asarray(a, dtype=np.float32)
+    import torch
+
+    return torch.as_tensor(a, dtype=torch.float32, device=canvas.device)
+
+
+def _scatter(canvas, ids, part) -> None:
+    if isinstance(canvas, np.ndarray):
+        canvas[ids] = part
+    else:
+        import torch
+
+        idx = torch.as_tensor(ids, device=canvas.device)
+        canvas.index_copy_(0, idx, _as_like(canvas, part))
