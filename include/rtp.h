@@ -137,8 +137,11 @@ rtp_status rtp_write_pnm(const char* path, const float* rgba, int32_t nx, int32_
 
 /* CornellBox::buildDataSet.  variant 0: the reference scene (glass sphere
  * outside the box); 1: sphere at (190,90,190) (notebook cell 2; overlaps the
- * tall box); 2: sphere floating at (440,200,150), clear of the boxes.  The
- * returned descriptor points into library-owned static storage. */
+ * tall box); 2: sphere floating at (440,200,150), clear of the boxes;
+ * 3: the C3 stress scene -- the six walls with the light and 1000 spheres
+ * (sphere 0: glass at (190,90,190), the light-sphere target; spheres 1..999
+ * from the reference's RNG, see oracle/rtp_oracle.h for the exact recipe).
+ * The returned descriptor points into library-owned static storage. */
 rtp_status rtp_cornell_box(int32_t variant, rtp_scene_desc* out);
 
 /* Diagnostics: evaluate a device primitive elementwise (tests only).
@@ -157,7 +160,9 @@ int32_t rtp_debug_counters(rtp_context* ctx, uint64_t* out, int32_t n_out);
 /* Diagnostics: exhaustively compare a fast device arithmetic sequence with the
  * IEEE operation for every float bit pattern in [lo_bits, hi_bits].  kind 0:
  * rcp (v_rcp + 1 Newton step) vs 1.0f/x; 1: rcp + remainder correction; 2:
- * fast sqrt vs sqrtf; 3/4: 1/sqrt with rcp kind 0/1.  *mismatches = count,
+ * fast sqrt vs sqrtf; 3/4: 1/sqrt with rcp kind 0/1; 5: (float)(x*(1/pi)) vs
+ * (float)(x/pi) in double; 6/7: the branch-free sincos vs the sinf/cosf
+ * ports.  *mismatches = count,
  * *first_bad = smallest mismatching bit pattern (0xffffffff if none). */
 rtp_status rtp_verify_fast_math(rtp_context* ctx, int32_t kind, uint32_t lo_bits, uint32_t hi_bits,
                                 uint64_t* mismatches, uint32_t* first_bad);

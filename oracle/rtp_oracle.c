@@ -398,6 +398,47 @@ void rtpo_cornell_box(int32_t variant, rtpo_scene* s) {
   /* back wall (:247-258) */
   set4(p, 0, 0, 555, 555, 0, 555, 555, 555, 555, 0, 555, 555);
   cb_quad(s, &cell, p, 1, 1, 1);
+  if (variant == 3) { /* C3 scene (rtp_oracle.h) */
+    s->light_box_pointids[0] = 0;
+    s->light_box_pointids[1] = 8;
+    s->light_box_pointids[2] = 9;
+    s->light_box_pointids[3] = 10;
+    s->light_box_pointids[4] = 11;
+    s->light_sphere_point = s->n_points; /* sphere 0 centre */
+    s->ior = 1.5f;
+    uint32_t st = RTPO_C3_SEED;
+    for (int k = 0; k < RTPO_C3_SPHERES; k++) {
+      float cx = 190, cy = 90, cz = 190, rad = 90;
+      int mat = 4, tex = 0;
+      if (k > 0) {
+        float u4, u5;
+        for (;;) { /* redraw spheres that would intersect sphere 0 */
+          const float u0 = rtpo_randf(&st), u1 = rtpo_randf(&st), u2 = rtpo_randf(&st);
+          const float u3 = rtpo_randf(&st);
+          u4 = rtpo_randf(&st);
+          u5 = rtpo_randf(&st);
+          rad = 8.0f + 22.0f * u3;
+          cx = rad + (555.0f - 2.0f * rad) * u0;
+          cy = rad + (555.0f - 2.0f * rad) * u1;
+          cz = rad + (555.0f - 2.0f * rad) * u2;
+          const float dx = cx - 190.0f, dy = cy - 90.0f, dz = cz - 190.0f, g = 92.0f + rad;
+          if (!(dx * dx + dy * dy + dz * dz < g * g)) break;
+        }
+        if (u4 < 0.8f) {
+          mat = (int)(3.0f * u5);
+          if (mat > 2) mat = 2;
+          tex = mat;
+        }
+      }
+      s->sphere_point[k] = s->n_points;
+      cb_push_point(s, d555(cx), d555(cy), d555(cz));
+      s->sphere_radius[k] = d555(rad);
+      s->sphere_mat[k] = mat;
+      s->sphere_tex[k] = tex;
+    }
+    s->n_spheres = RTPO_C3_SPHERES;
+    return;
+  }
   /* small rotated box (:262-353) incl. the y=333 vertex typo (:327) */
   set4(p, 0, 0, 165, 165, 0, 165, 165, 330, 165, 0, 330, 165);
   cb_invert(p);

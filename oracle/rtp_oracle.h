@@ -68,7 +68,22 @@ void rtpo_camera_setup(const float pos[3], const float look_at[3], const float u
  *            dielectric path is exercised (it overlaps the tall box: most
  *            pixels NaN-poison, a stress case for the NaN semantics).
  * variant 2: sphere floating at (440,200,150), clear of every box (a clean
- *            visible glass sphere). */
+ *            visible glass sphere).
+ * variant 3: the C3 stress scene (BASELINE.json configs[2], SURVEY.md 8(d);
+ *            build-defined because the reference's SphereExtractor breaks for
+ *            more than one sphere): the six walls with the light, no boxes,
+ *            RTPO_C3_SPHERES spheres.  Sphere 0 is the glass sphere at the
+ *            notebook position (190,90,190), radius 90 (the light-sphere target
+ *            of the mixture pdf).  Spheres 1.. draw u0..u5 from the reference's
+ *            own RNG (getRandF, seed RTPO_C3_SEED) and set, in 555-units and
+ *            float arithmetic: r = 8 + 22*u3, centre_k = r + (555 - 2r)*u_k;
+ *            a sphere with |centre - (190,90,190)|^2 < (92 + r)^2 is redrawn
+ *            (a hit point inside the light sphere makes the reference's
+ *            sphere sampler NaN and poisons the pixel); u4 < 0.8: lambertian
+ *            matIdx = texIdx = min(2, int(3*u5)), else dielectric (4, 0).
+ *            Coordinates are then /555.0 in double. */
+#define RTPO_C3_SPHERES 1000
+#define RTPO_C3_SEED 3u
 void rtpo_cornell_box(int32_t variant, rtpo_scene* out);
 
 /* Scalar per-pixel render of an arbitrary pixel subset (pixels are fully

@@ -19,8 +19,8 @@
 #include "../../include/rtp.h"
 #include "rtp_layout.hpp"
 
-extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int* variant_out, int* waves_out);
-extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::KParams* p, int variant, int waves,
+extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int bvh, int* variant_out, int* waves_out);
+extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::KParams* p, int variant, int waves, int bvh,
                                         hipStream_t stream);
 extern "C" hipError_t rtp_launch_eval_primitive(int kind, const void* in, void* out, int64_t n, hipStream_t stream);
 extern "C" hipError_t rtp_launch_verify_fast_math(int kind, uint32_t lo, uint64_t count, unsigned long long* bad,
@@ -106,6 +106,55 @@ void fill_quad(rtp::DevQuad& Q, v3 q, v3 r, v3 s, v3 t) {
 
 bool bit_equal(const float* a, const float* b, int n) { return std::memcmp(a, b, sizeof(float) * n) == 0; }
 
+// Sphere BVH (replaces the VTK-m LinearBVH of buildBVH, MapperPathTracer.cxx:
+// 437-449, for scenes with many spheres).  Median split on the longest axis
+// of the centroid bounds, ties broken by sphere index (deterministic), leaves
+// of <= kBvhLeafSize spheres, depth-first "threaded" layout.  The boxes only
+// cull: each sphere box is padded by 0.2% of its radius + 1e-5 so that every
+// point the device's float sphere test can return lies inside it, and the
+// kernel compares against a slack-widened [0, t_best] interval.  The closest
+// hit is the lexicographic min of (t, kind, index) whatever the visit order.
+struct BvhPrim {
+  float lo[3], hi[3], cen[3];
+  int32_t idx;
+};
+
+int32_t bvh_build(std::vector<BvhPrim>& P, int b, int e, std::vector<rtp::BvhNode>& out, std::vector<int32_t>& order) {
+  const int32_t me = (int32_t)out.size();
+  out.push_back(rtp::BvhNode{});
+  rtp::BvhNode nd{};
+  float clo[3], chi[3];
+  for (int k = 0; k < 3; k++) {
+    nd.lo[k] = clo[k] = INFINITY;
+    nd.hi[k] = chi[k] = -INFINITY;
+  }
+  for (int i = b; i < e; i++)
+    for (int k = 0; k < 3; k++) {
+      nd.lo[k] = std::min(nd.lo[k], P[i].lo[k]);
+      nd.hi[k] = std::max(nd.hi[k], P[i].hi[k]);
+      clo[k] = std::min(clo[k], P[i].cen[k]);
+      chi[k] = std::max(chi[k], P[i].cen[k]);
+    }
+  if (e - b <= rtp::kBvhLeafSize) {
+    nd.leaf = ((int32_t)order.size() << 3) | (e - b);
+    for (int i = b; i < e; i++) order.push_back(P[i].idx);
+  } else {
+    int ax = 0;
+    for (int k = 1; k < 3; k++)
+      if (chi[k] - clo[k] > chi[ax] - clo[ax]) ax = k;
+    std::sort(P.begin() + b, P.begin() + e, [ax](const BvhPrim& x, const BvhPrim& y) {
+      return x.cen[ax] < y.cen[ax] || (x.cen[ax] == y.cen[ax] && x.idx < y.idx);
+    });
+    const int mid = b + (e - b) / 2;
+    bvh_build(P, b, mid, out, order);
+    bvh_build(P, mid, e, out, order);
+    nd.leaf = 0;
+  }
+  nd.skip = (int32_t)out.size();
+  out[me] = nd;
+  return me;
+}
+
 }  // namespace
 
 struct rtp_context {
@@ -117,6 +166,11 @@ struct rtp_context {
   unsigned long long* d_dbg = nullptr;  // RTP_DEBUG_STATS=1: per-wave counters of the last launch
   int dbg_waves = 0;
   unsigned long long* d_progress = nullptr;  // global finished-sample counter of the pool kernel
+  // many-sphere scenes: threaded BVH + sphere records (rtp_layout.hpp)
+  rtp::BvhNode* d_nodes = nullptr;
+  rtp::DevSphereG* d_sph_geom = nullptr;
+  rtp::DevSphere* d_sph_all = nullptr;
+  bool use_bvh = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
@@ -159,6 +213,9 @@ void rtp_destroy(rtp_context* c) {
   if (c->d_hist) hipFree(c->d_hist);
   if (c->d_dbg) hipFree(c->d_dbg);
   if (c->d_progress) hipFree(c->d_progress);
+  if (c->d_nodes) hipFree(c->d_nodes);
+  if (c->d_sph_geom) hipFree(c->d_sph_geom);
+  if (c->d_sph_all) hipFree(c->d_sph_all);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
   delete c;
@@ -173,7 +230,7 @@ void rtp_destroy(rtp_context* c) {
 rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
   if (!c || !s) return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_set_scene: NULL argument");
   if (s->n_points <= 0 || !s->points) return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_set_scene: no points");
-  if (s->n_quads < 0 || s->n_spheres < 0 || s->n_spheres > rtp::kMaxSpheres)
+  if (s->n_quads < 0 || s->n_spheres < 0 || s->n_spheres > rtp::kMaxSpheresBvh)
     return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_set_scene: bad primitive counts");
   if (s->n_spheres < 1)
     return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_set_scene: the light sphere radius is SphereRadii[0]; need >= 1 sphere");
@@ -235,17 +292,49 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     h->kind_begin[7] = pos;
   }
   h->n_quads = (int32_t)kept.size();
+  std::vector<rtp::DevSphere> sph(s->n_spheres);
   for (int k = 0; k < s->n_spheres; k++) {
-    if (!pt_ok(s->sphere_point[k]) || !mat_ok(s->sphere_mat[k]) || !tex_ok(s->sphere_tex[k])) {
+    if (!pt_ok(s->sphere_point[k]) || !mat_ok(s->sphere_mat[k]) || !tex_ok(s->sphere_tex[k]) ||
+        !(s->sphere_radius[k] > 0.0f)) {
       delete h;
-      return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_set_scene: sphere index out of range");
+      return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_set_scene: sphere index or radius out of range");
     }
-    rtp::DevSphere& S = h->spheres[k];
+    rtp::DevSphere& S = sph[k];
+    std::memset(&S, 0, sizeof(S));
     st(S.c, ld(s->points + 3 * s->sphere_point[k]));
     S.r = s->sphere_radius[k];
     S.rr = S.r * S.r;
     S.mt = s->mat_type[s->sphere_mat[k]];
     st(S.alb, ld(s->tex_rgb + 3 * s->tex_type[s->sphere_tex[k]]));
+  }
+  const bool use_bvh = s->n_spheres >= rtp::kBvhMinSpheres;
+  std::vector<rtp::BvhNode> nodes;
+  std::vector<rtp::DevSphereG> geom;
+  if (!use_bvh) {
+    for (int k = 0; k < s->n_spheres; k++) h->spheres[k] = sph[k];
+  } else {
+    std::vector<BvhPrim> P(s->n_spheres);
+    for (int k = 0; k < s->n_spheres; k++) {
+      const rtp::DevSphere& S = sph[k];
+      const float pad = 0.002f * S.r + 1e-5f;
+      for (int a = 0; a < 3; a++) {
+        P[k].lo[a] = S.c[a] - S.r - pad;
+        P[k].hi[a] = S.c[a] + S.r + pad;
+        P[k].cen[a] = S.c[a];
+      }
+      P[k].idx = k;
+    }
+    std::vector<int32_t> order;
+    bvh_build(P, 0, s->n_spheres, nodes, order);
+    geom.resize(order.size());
+    for (size_t j = 0; j < order.size(); j++) {
+      const rtp::DevSphere& S = sph[order[j]];
+      std::memset(&geom[j], 0, sizeof(geom[j]));
+      std::memcpy(geom[j].c, S.c, sizeof(S.c));
+      geom[j].rr = S.rr;
+      geom[j].orig = order[j];
+    }
+    h->n_nodes = (int32_t)nodes.size();
   }
   h->n_spheres = s->n_spheres;
   // lights (MapperPathTracer.cxx:141-148): light quad = light_box_pointids[1..4]
@@ -275,14 +364,34 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     h->light.gz0 = z0, h->light.gdz = z1 - z0;
   }
   st(h->light.sc, ld(s->points + 3 * s->light_sphere_point));
-  h->light.sr = s->sphere_radius[0];
+  h->light.sr = s->sphere_radius[0];  // SphereRadii[0] (PdfWorklet.h:205-210)
   h->light.srr = h->light.sr * h->light.sr;
   h->ior = s->ior;
   h->which_t1 = which_threshold(2);
   h->which_t2 = which_threshold(3);
   hipError_t e = hipSetDevice(c->device);
+  for (void** p : {(void**)&c->d_nodes, (void**)&c->d_sph_geom, (void**)&c->d_sph_all})
+    if (*p && e == hipSuccess) {
+      e = hipFree(*p);
+      *p = nullptr;
+    }
+  if (use_bvh && e == hipSuccess) {
+    e = hipMalloc(&c->d_nodes, nodes.size() * sizeof(rtp::BvhNode));
+    if (e == hipSuccess) e = hipMalloc(&c->d_sph_geom, geom.size() * sizeof(rtp::DevSphereG));
+    if (e == hipSuccess) e = hipMalloc(&c->d_sph_all, sph.size() * sizeof(rtp::DevSphere));
+    if (e == hipSuccess)
+      e = hipMemcpy(c->d_nodes, nodes.data(), nodes.size() * sizeof(rtp::BvhNode), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+      e = hipMemcpy(c->d_sph_geom, geom.data(), geom.size() * sizeof(rtp::DevSphereG), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+      e = hipMemcpy(c->d_sph_all, sph.data(), sph.size() * sizeof(rtp::DevSphere), hipMemcpyHostToDevice);
+    h->nodes = c->d_nodes;
+    h->sph_geom = c->d_sph_geom;
+    h->sph_all = c->d_sph_all;
+  }
   if (e == hipSuccess) e = hipMemcpy(c->d_scene, h, sizeof(*h), hipMemcpyHostToDevice);
   delete h;
+  c->use_bvh = use_bvh;
   if (e != hipSuccess) return hip_fail(e, "rtp_set_scene upload");
   c->has_scene = true;
   return RTP_OK;
@@ -349,7 +458,7 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
   p.seed_out = d_seed;
   p.live_out = d_live;
   int variant = 2, waves = 0;
-  const int64_t lanes = rtp_plan_history_lanes(npix, &variant, &waves);
+  const int64_t lanes = rtp_plan_history_lanes(npix, c->use_bvh ? 1 : 0, &variant, &waves);
   size_t hist_need = (size_t)(depth > 1 ? depth - 1 : 1) * (size_t)lanes * 16;
   rtp_status rs = ensure_hist(c, hist_need);
   if (rs != RTP_OK) return rs;
@@ -369,7 +478,7 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
     }
   }
   if (kernel_ms) HIP_TRY(hipEventRecord(c->ev0, stream));
-  HIP_TRY(rtp_launch_render(c->d_scene, &p, variant, waves, stream));
+  HIP_TRY(rtp_launch_render(c->d_scene, &p, variant, waves, c->use_bvh ? 1 : 0, stream));
   if (kernel_ms) {
     HIP_TRY(hipEventRecord(c->ev1, stream));
     HIP_TRY(hipEventSynchronize(c->ev1));
@@ -532,7 +641,8 @@ rtp_status rtp_eval_primitive(rtp_context* c, int32_t kind, const void* in, void
 // see rtp_verify_fast_math_kernel) over float bit patterns [lo_bits, hi_bits].
 rtp_status rtp_verify_fast_math(rtp_context* c, int32_t kind, uint32_t lo_bits, uint32_t hi_bits,
                                 uint64_t* mismatches, uint32_t* first_bad) {
-  if (!c || !mismatches || hi_bits < lo_bits) return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_verify_fast_math: bad args");
+  if (!c || !mismatches || hi_bits < lo_bits || kind < 0 || kind > 7)
+    return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_verify_fast_math: bad args");
   HIP_TRY(hipSetDevice(c->device));
   unsigned long long* d_bad = nullptr;
   uint32_t* d_first = nullptr;

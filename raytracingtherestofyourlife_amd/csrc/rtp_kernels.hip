@@ -65,6 +65,70 @@ RTP_DEV void scan_aa(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d, 
   }
 }
 
+// SphereLeafIntersector::hit's accepted root without the tmax test: the
+// reference takes r1 = (-b-sq)/a if tmin < r1 < tmax, else r2 = (-b+sq)/a if
+// tmin < r2 < tmax.  r1 <= r2 (a > 0), so r1 >= tmax rules out r2 too: the
+// accepted root is "r1 if r1 > tmin else r2", accepted iff it is > tmin and
+// < tmax.  It does not depend on tmax, so spheres may be visited in any order.
+RTP_DEV bool sphere_root(f3 o, f3 d, float tmin, f3 c, float rr, float& t_out) {
+  f3 oc = sub(o, c);
+  float a = dot(d, d);
+  float b = dot(oc, d);
+  float cc = dot(oc, oc) - rr;
+  float disc = b * b - a * cc;
+  if (!(disc > 0)) return false;
+  float sq = sqrt_exact(b * b - a * cc);
+  float r1 = (-b - sq) / a;
+  float t = r1 > tmin ? r1 : (-b + sq) / a;
+  t_out = t;
+  return t > tmin;
+}
+
+// Threaded-BVH walk over the spheres (scenes with >= kBvhMinSpheres).  The
+// brute-force scan in index order with a strict '<' returns the
+// lexicographic minimum of (t, quads before spheres, sphere index); the walk
+// visits spheres in BVH order and keeps that minimum explicitly.  Node boxes
+// only cull (padded on the host; compared with slack here), so no sphere
+// whose root could win is skipped.
+RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
+  const float tmin = 0.001f;
+  const float ix = __builtin_amdgcn_rcpf(fabsf(d.x) < 1e-20f ? copysignf(1e-20f, d.x) : d.x);
+  const float iy = __builtin_amdgcn_rcpf(fabsf(d.y) < 1e-20f ? copysignf(1e-20f, d.y) : d.y);
+  const float iz = __builtin_amdgcn_rcpf(fabsf(d.z) < 1e-20f ? copysignf(1e-20f, d.z) : d.z);
+  const BvhNode* __restrict__ nodes = sc->nodes;
+  const DevSphereG* __restrict__ geom = sc->sph_geom;
+  const int nn = sc->n_nodes;
+  int ni = 0;
+  while (ni < nn) {
+    const float4 a = *reinterpret_cast<const float4*>(&nodes[ni].lo[0]);
+    const float4 b = *reinterpret_cast<const float4*>(&nodes[ni].hi[0]);
+    const float x0 = (a.x - o.x) * ix, x1 = (b.x - o.x) * ix;
+    const float y0 = (a.y - o.y) * iy, y1 = (b.y - o.y) * iy;
+    const float z0 = (a.z - o.z) * iz, z1 = (b.z - o.z) * iz;
+    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+    const float slack = 1e-5f * fabsf(tf) + 1e-7f;
+    const bool hit = tn <= tf + slack && tf >= 0.0f && tn <= h.t * 1.00001f + 1e-7f;
+    const int skip = __float_as_int(a.w), leaf = __float_as_int(b.w);
+    if (hit && leaf) {
+      const int first = leaf >> 3, cnt = leaf & 7;
+      for (int j = first; j < first + cnt; j++) {
+        const float4 g0 = *reinterpret_cast<const float4*>(&geom[j].c[0]);
+        const int orig = geom[j].orig;
+        float t;
+        if (sphere_root(o, d, tmin, mk(g0.x, g0.y, g0.z), g0.w, t) &&
+            (t < h.t || (t == h.t && h.kind == 1 && orig < h.idx))) {
+          h.t = t;
+          h.kind = 1;
+          h.idx = orig;
+        }
+      }
+    }
+    ni = (hit && !leaf) ? ni + 1 : skip;
+  }
+}
+
+template <bool kBvh>
 RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d) {
   Hit h{3.40282347e+38f, -1, 0};
   int best = 0x7fffffff;
@@ -87,14 +151,18 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d) {
       best = orig;
     }
   }
-  const int ns = sc->n_spheres;
-  for (int k = 0; k < ns; k++) {
-    const DevSphere& S = sc->spheres[k];
-    float t;
-    if (sphere_hit(o, d, tmin, h.t, ld3(S.c), S.rr, t)) {
-      h.t = t;
-      h.kind = 1;
-      h.idx = k;
+  if constexpr (kBvh) {
+    spheres_bvh(sc, o, d, h);
+  } else {
+    const int ns = sc->n_spheres;
+    for (int k = 0; k < ns; k++) {
+      const DevSphere& S = sc->spheres[k];
+      float t;
+      if (sphere_hit(o, d, tmin, h.t, ld3(S.c), S.rr, t)) {
+        h.t = t;
+        h.kind = 1;
+        h.idx = k;
+      }
     }
   }
   return h;
@@ -127,6 +195,7 @@ enum BounceResult { kAlive = 0, kMissed = 1, kLight = 2 };
 // (when d <= D-2).  On kLight, `emit` receives E[d].
 RTP_DEV unsigned long long stamp(bool on) { return on ? __builtin_amdgcn_s_memtime() : 0ull; }
 
+template <bool kBvh>
 RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3& emit, float4* __restrict__ hist_d,
                    int D, unsigned long long* dbg = nullptr) {
   const bool st = dbg != nullptr;
@@ -136,7 +205,7 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
   const f3 org = ps.org, dir = ps.dir;
   const int d = ps.d;
   // intersect + CollectIntersecttWorklet (SurfaceWorklets.h:104-109)
-  Hit h = closest_hit(sc, org, dir);
+  Hit h = closest_hit<kBvh>(sc, org, dir);
   if (st) {
     const unsigned long long t1s = __builtin_amdgcn_s_memtime();
     dbg[kDbgCyclesIntersect] += t1s - t0;
@@ -156,7 +225,7 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
     mt = Q.mt;
     alb = ld3(Q.alb);
   } else {
-    const DevSphere& S = sc->spheres[h.idx];
+    const DevSphere& S = kBvh ? sc->sph_all[h.idx] : sc->spheres[h.idx];
     hn = mk((hp.x - S.c[0]) / S.r, (hp.y - S.c[1]) / S.r, (hp.z - S.c[2]) / S.r);
     mt = S.mt;
     alb = ld3(S.alb);
@@ -291,6 +360,7 @@ RTP_DEV f3 path_radiance(int result, int k, f3 emit, bool nonfinite, const float
 RTP_DEV int64_t pixel_of(const KParams& p, int64_t k) { return p.pixel_ids ? p.pixel_ids[k] : p.pixel_begin + k; }
 
 // ------------------------------------------------------------------ v1 ---
+template <bool kBvh>
 __global__ void __launch_bounds__(256) rtp_render_lockstep(const DevScene* __restrict__ sc, KParams p) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= p.npix) return;
@@ -317,7 +387,7 @@ __global__ void __launch_bounds__(256) rtp_render_lockstep(const DevScene* __res
       }
       live++;
       ps.d = d;
-      result = bounce(sc, ps, seed, emit, hist + (int64_t)d * stride, D);
+      result = bounce<kBvh>(sc, ps, seed, emit, hist + (int64_t)d * stride, D);
       if (result != kAlive) k_end = d;
     }
     f3 c = path_radiance(result, k_end, emit, ps.nonfinite, hist, stride);
@@ -369,7 +439,7 @@ RTP_DEV void set_priority(float lag) {  // s_setprio needs an immediate
 #ifndef RTP_POOL_MIN_WAVES_PER_EU
 #define RTP_POOL_MIN_WAVES_PER_EU 4
 #endif
-template <bool kStats>
+template <bool kStats, bool kBvh>
 __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_pool(const DevScene* __restrict__ sc, KParams p, int n_waves) {
   __shared__ __align__(16) unsigned char smem[kPoolLdsBytes];
   const int lane = threadIdx.x & 63;
@@ -502,7 +572,7 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
     unsigned long long tbnc = ta;
     if (has_path) {
       f3 emit = mk(0.f, 0.f, 0.f);
-      const int res = bounce(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D, want_dbg ? dbg : nullptr);
+      const int res = bounce<kBvh>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D, want_dbg ? dbg : nullptr);
       tbnc = stamp(want_dbg);
       if (res == kAlive && ps.d < D - 1) {
         ps.d++;
@@ -594,6 +664,8 @@ __global__ void rtp_verify_fast_math_kernel(int kind, uint32_t lo, uint64_t coun
     case 3: want = 1.0f / __builtin_sqrtf(x); got = rcp_nr1(sqrt_fast(x)); break;
     case 4: want = 1.0f / __builtin_sqrtf(x); got = rcp_nr2(sqrt_fast(x)); break;
     case 5: want = (float)((double)x / kPi); got = cos_over_pi(x); break;
+    case 6: { float s, c; rtp_sincosf(x, &s, &c); want = rtp_sinf(x); got = s; break; }
+    case 7: { float s, c; rtp_sincosf(x, &s, &c); want = rtp_cosf(x); got = c; break; }
     default: break;
   }
   if (__float_as_uint(want) != __float_as_uint(got)) {
@@ -615,17 +687,25 @@ extern "C" hipError_t rtp_launch_verify_fast_math(int kind, uint32_t lo, uint64_
   return hipGetLastError();
 }
 namespace {
-int pool_resident_waves(bool stats) {
-  static int cached[2] = {-1, -1};
-  if (cached[stats] > 0) return cached[stats];
-  int dev = 0, cus = 0, nb = 0;
+template <bool kStats, bool kBvh>
+int resident_blocks_per_cu() {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtp::rtp_render_pool<kStats, kBvh>, 256, 0) != hipSuccess ||
+      nb <= 0)
+    nb = 1;
+  return nb;
+}
+int pool_resident_waves(bool stats, bool bvh) {
+  static int cached[2][2] = {{-1, -1}, {-1, -1}};
+  int& c = cached[stats][bvh];
+  if (c > 0) return c;
+  int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 1024;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  hipError_t e = stats ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtp::rtp_render_pool<true>, 256, 0)
-                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtp::rtp_render_pool<false>, 256, 0);
-  if (e != hipSuccess || nb <= 0) nb = 1;
-  cached[stats] = cus * nb * rtp::kWavesPerBlock;
-  return cached[stats];
+  const int nb = stats ? (bvh ? resident_blocks_per_cu<true, true>() : resident_blocks_per_cu<true, false>())
+                       : (bvh ? resident_blocks_per_cu<false, true>() : resident_blocks_per_cu<false, false>());
+  c = cus * nb * rtp::kWavesPerBlock;
+  return c;
 }
 int kernel_variant() {
   const char* e = getenv("RTP_KERNEL");
@@ -635,7 +715,7 @@ int kernel_variant() {
 }  // namespace
 
 // Work plan: how many lanes' worth of attenuation history the launch needs.
-extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int* variant_out, int* waves_out) {
+extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int bvh, int* variant_out, int* waves_out) {
   const int v = kernel_variant();
   if (variant_out) *variant_out = v;
   if (v == 1) {
@@ -645,7 +725,7 @@ extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int* variant_out, int* w
   const int64_t by_lanes = (npix + 63) / 64;
   const int64_t by_pool = (npix + rtp::kPool - 1) / rtp::kPool;
   const char* st = getenv("RTP_DEBUG_STATS");
-  int64_t W = std::min<int64_t>(by_lanes, pool_resident_waves(st && st[0] == '1'));
+  int64_t W = std::min<int64_t>(by_lanes, pool_resident_waves(st && st[0] == '1', bvh != 0));
   W = std::max<int64_t>(W, by_pool);
   W = std::max<int64_t>(W, 1);
   if (waves_out) *waves_out = (int)W;
@@ -653,18 +733,23 @@ extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int* variant_out, int* w
 }
 
 extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::KParams* p, int variant, int waves,
-                                        hipStream_t stream) {
+                                        int bvh, hipStream_t stream) {
   if (p->npix <= 0) return hipSuccess;
   if (variant == 1) {
     const int64_t grid = (p->npix + 255) / 256;
-    hipLaunchKernelGGL(rtp::rtp_render_lockstep, dim3((unsigned)grid), dim3(256), 0, stream, scene, *p);
+    if (bvh)
+      hipLaunchKernelGGL(rtp::rtp_render_lockstep<true>, dim3((unsigned)grid), dim3(256), 0, stream, scene, *p);
+    else
+      hipLaunchKernelGGL(rtp::rtp_render_lockstep<false>, dim3((unsigned)grid), dim3(256), 0, stream, scene, *p);
   } else {
     const int blocks = (waves + rtp::kWavesPerBlock - 1) / rtp::kWavesPerBlock;
     const char* st = getenv("RTP_DEBUG_STATS");
-    if (p->dbg && st && st[0] == '1')
-      hipLaunchKernelGGL(rtp::rtp_render_pool<true>, dim3((unsigned)blocks), dim3(256), 0, stream, scene, *p, waves);
-    else
-      hipLaunchKernelGGL(rtp::rtp_render_pool<false>, dim3((unsigned)blocks), dim3(256), 0, stream, scene, *p, waves);
+    const bool stats = p->dbg && st && st[0] == '1';
+    const dim3 g((unsigned)blocks), b(256);
+    if (stats && bvh) hipLaunchKernelGGL((rtp::rtp_render_pool<true, true>), g, b, 0, stream, scene, *p, waves);
+    else if (stats) hipLaunchKernelGGL((rtp::rtp_render_pool<true, false>), g, b, 0, stream, scene, *p, waves);
+    else if (bvh) hipLaunchKernelGGL((rtp::rtp_render_pool<false, true>), g, b, 0, stream, scene, *p, waves);
+    else hipLaunchKernelGGL((rtp::rtp_render_pool<false, false>), g, b, 0, stream, scene, *p, waves);
   }
   return hipGetLastError();
 }

@@ -11,7 +11,10 @@
 namespace rtp {
 
 constexpr int kMaxQuads = 256;
-constexpr int kMaxSpheres = 256;
+constexpr int kMaxSpheres = 256;          // held inline in DevScene (scalar loads)
+constexpr int kMaxSpheresBvh = 1 << 22;   // spheres behind the BVH (global memory)
+constexpr int kBvhMinSpheres = 9;         // scenes with more spheres use the BVH
+constexpr int kBvhLeafSize = 4;
 
 // One quad of the Lagae-Dutre test (Surface.h:31-161) with v00=q, v10=r,
 // v11=s, v01=t.  Read with uniform (scalar) loads.
@@ -38,6 +41,25 @@ struct alignas(16) DevSphere {
   int32_t pad[7];
 };
 
+// Sphere record in BVH leaf order (global memory, per-lane loads).
+struct alignas(16) DevSphereG {
+  float c[3];
+  float rr;      // radius*radius
+  int32_t orig;  // index in the scene's sphere order (tie-break, material lookup)
+  int32_t pad[3];
+};
+
+// Threaded (stackless) BVH node in depth-first order: on a hit of an inner
+// node traversal continues at i+1 (its left child); on a miss, or after a
+// leaf, at `skip` (the first node after this subtree; n_nodes ends the walk).
+// The boxes are padded so that culling is conservative (rtp_host.cpp).
+struct alignas(16) BvhNode {
+  float lo[3];
+  int32_t skip;
+  float hi[3];
+  int32_t leaf;  // 0: inner; else (first << 3) | count, count in 1..kBvhLeafSize
+};
+
 struct alignas(16) DevLights {
   DevQuad quad;   // light quad for QuadPDFWorklet (PdfWorklet.h:230-248)
   float area;     // Magnitude(r-q) * Magnitude(t-q)
@@ -58,7 +80,11 @@ struct alignas(16) DevScene {
   uint32_t which_t1;  // smallest hash with which >= 2   (PdfWorklet.h:20)
   uint32_t which_t2;  // smallest hash with which == 3
   float ior;
-  int32_t pad[3];
+  int32_t n_nodes;                 // BVH scenes (n_spheres >= kBvhMinSpheres)
+  int32_t pad[2];
+  const BvhNode* nodes;
+  const DevSphereG* sph_geom;      // BVH leaf order
+  const DevSphere* sph_all;        // scene order (materials of the hit sphere)
   DevLights light;
   DevQuad quads[kMaxQuads];
   DevSphere spheres[kMaxSpheres];

@@ -7,6 +7,7 @@
 //     float, transposed, pre-multiplied by Translate(265,0,295)
 //     (CornellBox::invert, :10-35)
 //   * buildBox's duplicated faces and the y=333 vertex typo are kept.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <mutex>
@@ -38,6 +39,19 @@ struct SceneStore {
 };
 
 using P4 = float[4][3];
+
+constexpr int kC3Spheres = 1000;
+constexpr uint32_t kC3Seed = 3u;
+
+// wangXor getRandF (wangXor.h:30-38, 55-59): float(t) / 4294967295.f == float(t) * 2^-32
+float draw(uint32_t& s) {
+  s = (s ^ 61u) ^ (s >> 16);
+  s *= 9u;
+  s = s ^ (s >> 4);
+  s *= 0x27d4eb2du;
+  s = s ^ (s >> 15);
+  return (float)s * 0x1p-32f;
+}
 
 void rect(P4& p, std::initializer_list<float> v) {
   auto it = v.begin();
@@ -105,6 +119,37 @@ void build(SceneStore& s, int variant) {
   s.add_quad(p, 1, 1);
   rect(p, {0, 0, 555, 555, 0, 555, 555, 555, 555, 0, 555, 555});  // back wall
   s.add_quad(p, 1, 1);
+  if (variant == 3) {  // C3 stress scene: walls + light + kC3Spheres spheres (rtp.h)
+    uint32_t st = kC3Seed;
+    for (int k = 0; k < kC3Spheres; k++) {
+      float cx = 190, cy = 90, cz = 190, rad = 90;
+      int mat = 4, tex = 0;
+      if (k > 0) {
+        float u4, u5;
+        for (;;) {  // redraw spheres that would intersect sphere 0
+          const float u0 = draw(st), u1 = draw(st), u2 = draw(st), u3 = draw(st);
+          u4 = draw(st);
+          u5 = draw(st);
+          rad = 8.0f + 22.0f * u3;
+          cx = rad + (555.0f - 2.0f * rad) * u0;
+          cy = rad + (555.0f - 2.0f * rad) * u1;
+          cz = rad + (555.0f - 2.0f * rad) * u2;
+          const float dx = cx - 190.0f, dy = cy - 90.0f, dz = cz - 190.0f, g = 92.0f + rad;
+          if (!(dx * dx + dy * dy + dz * dz < g * g)) break;
+        }
+        if (u4 < 0.8f) {
+          mat = std::min(2, (int)(3.0f * u5));
+          tex = mat;
+        }
+      }
+      s.sphere_point.push_back((int32_t)(s.points.size() / 3));
+      for (float v : {cx, cy, cz}) s.points.push_back((float)((double)v / 555.0));
+      s.sphere_radius.push_back((float)((double)rad / 555.0));
+      s.sphere_mat.push_back(mat);
+      s.sphere_tex.push_back(tex);
+    }
+    return;
+  }
   const std::initializer_list<float> small_box[6] = {
       {0, 0, 165, 165, 0, 165, 165, 330, 165, 0, 330, 165},  {0, 0, 0, 165, 0, 0, 165, 330, 0, 0, 330, 0},
       {165, 0, 0, 165, 330, 0, 165, 330, 165, 165, 0, 165},  {0, 0, 0, 0, 330, 0, 0, 330, 165, 0, 0, 165},
@@ -131,13 +176,13 @@ void build(SceneStore& s, int variant) {
   box(s, n2, f2);
 }
 
-SceneStore g_store[3];
-std::once_flag g_once[3];
+SceneStore g_store[4];
+std::once_flag g_once[4];
 
 }  // namespace
 
 extern "C" rtp_status rtp_cornell_box(int32_t variant, rtp_scene_desc* out) {
-  if (!out || variant < 0 || variant > 2) return RTP_ERR_INVALID_ARGUMENT;
+  if (!out || variant < 0 || variant > 3) return RTP_ERR_INVALID_ARGUMENT;
   std::call_once(g_once[variant], [variant] { build(g_store[variant], variant); });
   const SceneStore& s = g_store[variant];
   std::memset(out, 0, sizeof(*out));
@@ -163,7 +208,7 @@ extern "C" rtp_status rtp_cornell_box(int32_t variant, rtp_scene_desc* out) {
   out->light_quad_points[1] = 9;
   out->light_quad_points[2] = 10;
   out->light_quad_points[3] = 11;
-  out->light_sphere_point = 4 * 12;
+  out->light_sphere_point = s.sphere_point[0];  // 4 * 12 for variants 0..2
   out->ior = 1.5f;
   return RTP_OK;
 }

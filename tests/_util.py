@@ -41,3 +41,13 @@ def rmse_normalized(a_sum: np.ndarray, b_sum: np.ndarray, spp: int) -> float:
 
     d = norm(a_sum).astype(np.float64) - norm(b_sum).astype(np.float64)
     return float(np.sqrt(np.mean(d * d)))
+
+
+def set_scene_from_oracle(device, sc) -> None:
+    """Upload an oracle Scene (e.g. an edited cornell_box) through rtp_set_scene."""
+    nq, ns = sc.n_quads, sc.n_spheres
+    arr = np.ctypeslib.as_array
+    device.set_scene(sc.points_np(), sc.quad_ids_np()[:, 1:], arr(sc.quad_mat)[:nq], arr(sc.quad_tex)[:nq],
+                     arr(sc.sphere_point)[:ns], arr(sc.sphere_radius)[:ns], arr(sc.sphere_mat)[:ns],
+                     arr(sc.sphere_tex)[:ns], arr(sc.mat_type)[: sc.n_mat], arr(sc.tex_type)[: sc.n_tex_type],
+                     arr(sc.tex)[: sc.n_tex], tuple(sc.light_box_pointids[1:5]), sc.light_sphere_point, sc.ior)

@@ -51,7 +51,7 @@ def test_create_without_gpu_fails_cleanly():
     assert e.value.status == -3
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 def test_product_cornell_box_equals_oracle(oracle, variant):
     import raytracingtherestofyourlife_amd as rtp
 
@@ -62,8 +62,13 @@ def test_product_cornell_box_equals_oracle(oracle, variant):
     assert np.array_equal(cb.ds.cellset.quad_points, o.quad_ids_np()[:, 1:])
     assert np.array_equal(cb.matIdx[0], np.ctypeslib.as_array(o.quad_mat)[: o.n_quads])
     assert np.array_equal(cb.texIdx[0], np.ctypeslib.as_array(o.quad_tex)[: o.n_quads])
-    assert cb.ds.cellset.sphere_points.tolist() == [o.sphere_point[0]]
-    assert np.float32(cb.SphereRadii[0]).view(np.uint32) == np.float32(o.sphere_radius[0]).view(np.uint32)
+    ns = o.n_spheres
+    assert cb.ds.cellset.sphere_points.tolist() == list(o.sphere_point[:ns])
+    assert np.array_equal(cb.SphereRadii.view(np.uint32), np.ctypeslib.as_array(o.sphere_radius)[:ns].view(np.uint32))
+    assert np.array_equal(cb.matIdx[1], np.ctypeslib.as_array(o.sphere_mat)[:ns])
+    assert np.array_equal(cb.texIdx[1], np.ctypeslib.as_array(o.sphere_tex)[:ns])
+    assert list(cb.light_quad_points) == list(o.light_box_pointids[1:5])
+    assert cb.light_sphere_point == o.light_sphere_point
     assert np.array_equal(cb.tex.view(np.uint32), np.ctypeslib.as_array(o.tex)[:4].view(np.uint32))
     assert cb.matType.tolist() == [0, 0, 0, 1, 2] and cb.texType.tolist() == [0, 1, 2, 3, 0]
 
@@ -73,6 +78,7 @@ def test_bad_cornell_variant():
 
     d = rtp._lib.RtpSceneDesc()
     assert rtp.load().rtp_cornell_box(7, ctypes.byref(d)) == -1
+    assert rtp.load().rtp_cornell_box(4, ctypes.byref(d)) == -1
 
 
 def test_normalize_matches_oracle(oracle):

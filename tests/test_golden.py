@@ -22,7 +22,8 @@ def _load(name):
 
 
 def test_fixtures_present():
-    assert {"c1_full", "c2_subset", "c4_subset", "glass_subset", "glass2_subset", "c5_shard3_subset"} <= set(RENDERS)
+    assert {"c1_full", "c2_subset", "c3_subset", "c4_subset", "glass_subset", "glass2_subset",
+            "c5_shard3_subset"} <= set(RENDERS)
 
 
 def test_kat_json(oracle):

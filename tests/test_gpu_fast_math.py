@@ -29,3 +29,11 @@ def test_cos_over_pi_product_exact(device):
     """(float)((double)c * (1/pi)) == (float)((double)c / pi) for every float c in [0, 2]."""
     bad, first = device.verify_fast_math(5, 0.0, 2.0)
     assert bad == 0, f"cos_over_pi: {bad} mismatches, first bit pattern {first:#x}"
+
+
+@pytest.mark.parametrize("kind,name", [(6, "sin"), (7, "cos")])
+def test_branch_free_sincos_equals_ports(device, kind, name):
+    """rtp_sincosf (the generator's shared sincos) == rtp_sinf / rtp_cosf for
+    every float in [0, 2pi] (phi = float(2*pi*r), r in [0, 1])."""
+    bad, first = device.verify_fast_math(kind, 0.0, 6.2831855)
+    assert bad == 0, f"sincos/{name}: {bad} mismatches, first bit pattern {first:#x}"

@@ -8,7 +8,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from _util import assert_render_equal, rmse_normalized
+from _util import assert_render_equal, rmse_normalized, set_scene_from_oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -188,3 +188,33 @@ def test_invalid_arguments(device, rtp):
         device.render(bad, 4, 4, 1, 1)
     with pytest.raises(rtp.RtpError):
         device.render_pixels(cam, 4, 4, 1, 1, np.array([16], dtype=np.int64))
+
+
+def test_c3_many_spheres_bvh_subset(oracle, device, rtp):
+    """C3 geometry (2048x2048, 1000 spheres behind the BVH, depth 50): random
+    pixel subset at full depth against the brute-force oracle."""
+    nx = ny = 2048
+    pix = np.sort(np.random.default_rng(33).choice(nx * ny, size=384, replace=False)).astype(np.int64)
+    got, want = _render_both(oracle, device, rtp, 3, nx, ny, 4, 50, pix)
+    assert_render_equal(got, want, "c3")
+    assert (want[2] > 4).any()
+
+
+@pytest.mark.parametrize("n", [2, 8, 9, 40])
+def test_sphere_count_threshold_and_coincident_tie(oracle, device, rtp, n):
+    """Below, at and above the BVH threshold (kBvhMinSpheres = 9), with the
+    last sphere coincident with sphere 1 but another material: the reference's
+    index-order scan keeps the lower index on equal t, and so must the BVH."""
+    sc = oracle.cornell_box(3)
+    sc.n_spheres = n
+    sc.sphere_point[n - 1] = sc.sphere_point[1]
+    sc.sphere_radius[n - 1] = sc.sphere_radius[1]
+    sc.sphere_mat[n - 1] = 4 if sc.sphere_mat[1] != 4 else 1
+    sc.sphere_tex[n - 1] = 0
+    set_scene_from_oracle(device, sc)
+    nx, ny = 96, 96
+    cam = rtp.default_camera()
+    pix = np.arange(nx * ny, dtype=np.int64)
+    got = device.render_pixels(cam, nx, ny, 4, 12, pix)[:3]
+    want = oracle.render_pixels(sc, oracle.camera_setup(nx, ny), nx, ny, 4, 12, pix)
+    assert_render_equal(got, want, f"{n} spheres")

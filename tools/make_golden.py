@@ -3,7 +3,8 @@ oracle (oracle/rtp_oracle.c).  The reference itself cannot be built here (it
 needs VTK-m), so these are known-answer vectors of the restatement; see
 DESIGN.md "Parity".
 
-    python tools/make_golden.py            # all fixtures (~1-2 min, 8 cores)
+    python tools/make_golden.py            # all fixtures (a few minutes, 8 cores)
+    python tools/make_golden.py c3_subset  # only the named fixtures
 """
 from __future__ import annotations
 
@@ -30,7 +31,12 @@ def subset(n_total, k, seed):
     return np.sort(rng.choice(n_total, size=k, replace=False)).astype(np.int64)
 
 
+ONLY = set(sys.argv[1:])
+
+
 def render_fixture(name, variant, nx, ny, spp, depth, pixels=None, seed_base=0, camera=None):
+    if ONLY and name not in ONLY:
+        return
     t = time.time()
     sc = oc.cornell_box(variant)
     cam = oc.camera_setup(nx, ny, **(camera or {}))
@@ -71,8 +77,9 @@ def main():
     phis = np.float32([0.0, 0.5, 0.7853982, 1.0, 2.0, 3.1415927, 4.0, 5.5, 6.2831855])
     kat["sinf"] = {float(p).hex(): float(L.rtpo_sinf(float(p))).hex() for p in phis}
     kat["cosf"] = {float(p).hex(): float(L.rtpo_cosf(float(p))).hex() for p in phis}
-    with open(os.path.join(OUT, "kat.json"), "w") as f:
-        json.dump(kat, f, indent=1)
+    if not ONLY or "kat" in ONLY:
+        with open(os.path.join(OUT, "kat.json"), "w") as f:
+            json.dump(kat, f, indent=1)
     # --- renders ---------------------------------------------------------
     # C1 (BASELINE configs[0]): full image
     render_fixture("c1_full", 0, 200, 200, 10, 10)
@@ -86,6 +93,8 @@ def main():
     # sample-batch shard stream: seed_base = k*N for shard k = 3 of C5 geometry
     render_fixture("c5_shard3_subset", 0, 3840, 2160, 16, 50, pixels=subset(3840 * 2160, 512, 8),
                    seed_base=(3 * 3840 * 2160) % (1 << 32))
+    # C3 (BASELINE configs[2]): 1000-sphere scene, 2048x2048, 256 spp, depth 50 (assumed)
+    render_fixture("c3_subset", 3, 2048, 2048, 256, 50, pixels=subset(2048 * 2048, 1024, 12))
 
 
 if __name__ == "__main__":

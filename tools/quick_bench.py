@@ -11,9 +11,10 @@ ap.add_argument("--ny", type=int, default=800)
 ap.add_argument("--spp", type=int, default=50)
 ap.add_argument("--depth", type=int, default=50)
 ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--variant", type=int, default=0)
 a = ap.parse_args()
 dev = rtp.Device(0)
-dev.set_cornell_box(0)
+dev.set_cornell_box(a.variant)
 cam = rtp.default_camera()
 n = a.nx * a.ny
 out = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
