@@ -31,6 +31,9 @@
 
 #include "rtp_device.hpp"
 
+#ifndef RTP_FAIR_READY
+#define RTP_FAIR_READY 1  // pool kernel: lagging pixels jump the READY queue
+#endif
 #ifndef RTP_MERGED_GEN
 #define RTP_MERGED_GEN 1  // branch-free generator pass (bounce); 0: the three divergent branches
 #endif
@@ -476,6 +479,8 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
   wave_sync();
   // wave-uniform, monotone queue cursors
   int ready_head = 0, ready_tail = (S > 0) ? n_slots : 0, ff_head = 0, ff_tail = 0;
+  int unfinished = n_slots;                // stats only: pixels with samples still to run
+  unsigned long long t_tail = 0;
 
   float4* __restrict__ hist = reinterpret_cast<float4*>(p.hist) + ((int64_t)w * 64 + lane);  // [d][lane]
   const int64_t stride = (int64_t)n_waves * 64;
@@ -533,9 +538,25 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
         s_seed[fslot] = fseed;
         again = s_samples[fslot] < (uint32_t)S;
       }
+      if (want_dbg) unfinished -= __popcll(__ballot(mine && !again));
+#if RTP_FAIR_READY
+      // Fair share: a pixel whose completed samples are at or below the
+      // wave's average (ff_tail / n_slots) goes to the FRONT of the READY
+      // ring, the others to the back.  FIFO alone let cheap pixels (short
+      // paths, back sooner) take more than their share of lanes, so the
+      // expensive pixels' sequential sample chains ran on alone at the end
+      // (17% of bounce steps with ~12 of 64 lanes live).
+      const bool urgent = again && (uint64_t)s_samples[fslot] * (uint64_t)n_slots <= (uint64_t)ff_tail;
+      const uint64_t pu = __ballot(urgent), pn = __ballot(again && !urgent);
+      ready_head -= __popcll(pu);
+      if (urgent) q_ready[(ready_head + (int)lane_rank(pu)) & (kPool - 1)] = (uint16_t)fslot;
+      if (again && !urgent) q_ready[(ready_tail + (int)lane_rank(pn)) & (kPool - 1)] = (uint16_t)fslot;
+      ready_tail += __popcll(pn);
+#else
       const uint64_t push = __ballot(again);
       if (again) q_ready[(ready_tail + (int)lane_rank(push)) & (kPool - 1)] = (uint16_t)fslot;
       ready_tail += __popcll(push);
+#endif
       ff_head += n;
       wave_sync();
       if (want_dbg) {
@@ -608,6 +629,11 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
       // completed fractions: global g / (npix*S) vs own ff_tail / (n_slots*S)
       set_priority(((float)g / (float)p.npix - (float)ff_tail / (float)n_slots) / (float)S);
     }
+    if (want_dbg && unfinished < 64) {
+      if (t_tail == 0) t_tail = __builtin_amdgcn_s_memtime();
+      dbg[kDbgTailSteps] += 1;
+      dbg[kDbgTailLanes] += (unsigned long long)__popcll(__ballot(has_path || ended));
+    }
     if (want_dbg) {
       dbg[kDbgBounceSteps] += 1;
       dbg[kDbgBounceLanes] += (unsigned long long)__popcll(__ballot(has_path || ended));
@@ -619,6 +645,7 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
   if (want_dbg && lane == 0) {
     dbg[kDbgCyclesTotal] = __builtin_amdgcn_s_memtime() - t_start;
     dbg[kDbgRealEnd] = __builtin_amdgcn_s_memrealtime();
+    dbg[kDbgTailCycles] = t_tail ? __builtin_amdgcn_s_memtime() - t_tail : 0;
     for (int c = 0; c < (kStats ? kDbgCounters : 0); c++)
       if (c != kDbgRealStart && c != kDbgHwId) p.dbg[(int64_t)w * kDbgCounters + c] = dbg[c];
   }

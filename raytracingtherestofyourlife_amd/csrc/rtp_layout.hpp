@@ -127,6 +127,9 @@ enum DbgCounter {
   kDbgRealStart,         // s_memrealtime (100 MHz, chip-wide) at wave start (raw, not summed)
   kDbgRealEnd,           // ... at wave end
   kDbgHwId,              // HW_REG_HW_ID of the wave (SIMD/CU/SE placement)
+  kDbgTailSteps,         // bounce steps taken while < 64 of the wave's pixels were unfinished
+  kDbgTailLanes,         // live lanes summed over those steps
+  kDbgTailCycles,        // s_memtime cycles from the first such step to the wave's end
   kDbgCounters
 };
 

@@ -279,7 +279,8 @@ class Device:
 
     DEBUG_COUNTERS = ("bounce_steps", "bounce_lanes", "ff_phases", "ff_lanes", "ff_iters", "cycles_bounce",
                       "cycles_ff", "cycles_total", "cycles_intersect", "cycles_bounce_call", "cycles_end",
-                      "cycles_refill", "real_start", "real_end", "hw_id", "max_wave_cycles")
+                      "cycles_refill", "real_start", "real_end", "hw_id", "tail_steps", "tail_lanes",
+                      "tail_cycles", "max_wave_cycles")
 
     def debug_counters(self) -> dict:
         """Pool-kernel counters of the last launch made with RTP_DEBUG_STATS=1."""

@@ -26,5 +26,7 @@ for r in range(a.reps):
     torch.cuda.synchronize()
     wall = time.time() - t
     L = live.to(torch.int64).sum().item() / (n * a.spp)
+    Lp = (live.to(torch.float64) / a.spp).cpu().numpy()
     print(json.dumps(dict(rep=r, kernel_ms=st.kernel_ms, wall_s=wall, msamples_per_s=n * a.spp / (st.kernel_ms / 1e3) / 1e6,
-                          live_per_sample=L, nan_px=int(torch.isnan(out[:, :3]).any(1).sum().item()))), flush=True)
+                          live_per_sample=L, nan_px=int(torch.isnan(out[:, :3]).any(1).sum().item()),
+                          L_pixel_pct={q: round(float(np.percentile(Lp, q)), 3) for q in (50, 90, 99, 99.9, 100)})), flush=True)
