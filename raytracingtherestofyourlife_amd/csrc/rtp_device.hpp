@@ -248,70 +248,66 @@ RTP_DEV f3 local(const Onb& o, f3 a) {  // onb.h:27-28
 // Branch-free form: every rejection test of the reference is evaluated on the
 // same values and the hit is their conjunction (the early returns only skip
 // work, they never change a value that a later test reads).
-RTP_DEV bool quad_hit_general(const DevQuad& Q, f3 o, f3 d, float& t_out) {
-  const f3 e03 = ld3(Q.e03), e01 = ld3(Q.e01);
-  f3 P = cross(d, e03);
-  float det = dot(e01, P);
-  float inv_det = rcp_det(det);
-  f3 T = sub(o, ld3(Q.v00));
-  float alpha = dot(T, P) * inv_det;
-  f3 Qv = cross(T, e01);
-  float beta = dot(d, Qv) * inv_det;
-  float t = dot(e03, Qv) * inv_det;
-  bool ok = !(fabsf(det) < kEps) && !(alpha < 0.0f) && !(beta < 0.0f) && !(t < 0.0f);
-  if (ok && (alpha + beta) > 1.0f) {
-    const f3 e23 = ld3(Q.e23), e21 = ld3(Q.e21);
-    f3 Pp = cross(d, e21);
-    float detp = dot(e23, Pp);
-    float inv_detp = rcp_det(detp);
-    f3 Tp = sub(o, ld3(Q.v11));
-    float ap = dot(Tp, Pp) * inv_detp;
-    f3 Qp = cross(Tp, e23);
-    float bp = dot(d, Qp) * inv_detp;
-    ok = !(fabsf(detp) < kEps) && !(ap < 0.0f) && !(bp < 0.0f);
-  }
-  t_out = t;
-  return ok;
+//
+// Zero structure.  The edge vectors of most quads have exactly-zero
+// components (axis-aligned walls, faces of boxes rotated about y).  The
+// reference still multiplies by them; those products are +-0, and in a
+// left-to-right sum x + (+-0) == x, (+-0) - x == -x for x != 0.  Dropping
+// them can only change the SIGN of a zero result, and every such value only
+// reaches a comparison with 0 (== for both zeros), a sum with a nonzero term,
+// or a product that again only reaches such comparisons (det == +-0 is
+// rejected by |det| < eps before its reciprocal matters).  Inputs are finite
+// (ray directions are de-NaN'd / bounded, origins are hit points), so 0*x is
+// +-0.  Hence every nonzero intermediate is bit-identical to the full form.
+// M* are the compile-time masks of the nonzero edge components
+// (rtp_layout.hpp kQuadKind); two-term sums are order-free (commutative).
+constexpr int cross_mask(int me) {  // nonzero components of cross(full, e)
+  return (((me >> 1) | (me >> 2)) & 1) | ((((me >> 2) | me) & 1) << 1) | (((me | (me >> 1)) & 1) << 2);
+}
+template <int ME, int I>
+RTP_DEV float cross_c(const float (&a)[3], const float* e) {  // component I of cross(a, e)
+  constexpr int i1 = (I + 1) % 3, i2 = (I + 2) % 3;
+  constexpr bool p = (ME >> i2) & 1, q = (ME >> i1) & 1;
+  if constexpr (p && q) return a[i1] * e[i2] - a[i2] * e[i1];
+  else if constexpr (p) return a[i1] * e[i2];
+  else if constexpr (q) return -(a[i2] * e[i1]);
+  else return 0.0f;
+}
+template <int M>
+RTP_DEV float dot_m(const float* x, const float* y) {  // vtkm::Dot without the structural-zero terms
+  constexpr bool b0 = M & 1, b1 = (M >> 1) & 1, b2 = (M >> 2) & 1;
+  if constexpr (b0 && b1 && b2) return (x[0] * y[0] + x[1] * y[1]) + x[2] * y[2];
+  else if constexpr (b0 && b1) return x[0] * y[0] + x[1] * y[1];
+  else if constexpr (b0 && b2) return x[0] * y[0] + x[2] * y[2];
+  else if constexpr (b1 && b2) return x[1] * y[1] + x[2] * y[2];
+  else if constexpr (b0) return x[0] * y[0];
+  else if constexpr (b1) return x[1] * y[1];
+  else if constexpr (b2) return x[2] * y[2];
+  else return 0.0f;
 }
 
-// Axis-aligned rectangle: e01 = a*e_I, e03 = b*e_J, e21 = b2*e_J, e23 =
-// a2*e_I (classified on the host from exact zeros).  The reference's products
-// with the exactly-zero edge components are +-0, and x + (+-0) == x,
-// x - (+-0) == x, (+-0) - x == -x for x != 0; every zero-valued intermediate
-// only ever reaches a comparison or a product, so its sign is irrelevant.
-// Each nonzero intermediate is therefore bit-identical to the general form,
-// and two-term sums are order-free, so this computes the same hit and t.
-template <int I, int J>
-RTP_DEV bool quad_hit_aa(const DevQuad& Q, f3 o, f3 d, float& t_out) {
-  constexpr int J1 = (J + 1) % 3, J2 = (J + 2) % 3, I1 = (I + 1) % 3, I2 = (I + 2) % 3;
-  const float a = Q.a, b = Q.b;
+template <int K>
+RTP_DEV bool quad_hit_masked(const DevQuad& Q, f3 o, f3 d, float& t_out) {
+  constexpr int M01 = kQuadKind[K].m01, M03 = kQuadKind[K].m03, M21 = kQuadKind[K].m21, M23 = kQuadKind[K].m23;
+  constexpr int MP = cross_mask(M03), MQ = cross_mask(M01), MPp = cross_mask(M21), MQp = cross_mask(M23);
   const float dv[3] = {d.x, d.y, d.z};
-  const float Tv[3] = {o.x - Q.v00[0], o.y - Q.v00[1], o.z - Q.v00[2]};
-  float P[3] = {0.f, 0.f, 0.f};
-  P[J1] = dv[J2] * b;         // cross(d, b e_J)
-  P[J2] = -(dv[J1] * b);
-  const float det = a * P[I];  // dot(e01, P)
+  const float P[3] = {cross_c<M03, 0>(dv, Q.e03), cross_c<M03, 1>(dv, Q.e03), cross_c<M03, 2>(dv, Q.e03)};
+  const float det = dot_m<M01 & MP>(Q.e01, P);
   const float inv_det = rcp_det(det);
-  const float alpha = (Tv[J1] * P[J1] + Tv[J2] * P[J2]) * inv_det;
-  float Qv[3] = {0.f, 0.f, 0.f};
-  Qv[I1] = Tv[I2] * a;        // cross(T, a e_I)
-  Qv[I2] = -(Tv[I1] * a);
-  const float beta = (dv[I1] * Qv[I1] + dv[I2] * Qv[I2]) * inv_det;
-  const float t = (b * Qv[J]) * inv_det;  // dot(e03, Q) * inv_det
+  const float T[3] = {o.x - Q.v00[0], o.y - Q.v00[1], o.z - Q.v00[2]};
+  const float alpha = dot_m<MP>(T, P) * inv_det;
+  const float Qv[3] = {cross_c<M01, 0>(T, Q.e01), cross_c<M01, 1>(T, Q.e01), cross_c<M01, 2>(T, Q.e01)};
+  const float beta = dot_m<MQ>(dv, Qv) * inv_det;
+  const float t = dot_m<M03 & MQ>(Q.e03, Qv) * inv_det;
   bool ok = !(fabsf(det) < kEps) && !(alpha < 0.0f) && !(beta < 0.0f) && !(t < 0.0f);
   if (ok && (alpha + beta) > 1.0f) {
-    const float a2 = Q.a2, b2 = Q.b2;
-    const float Tp[3] = {o.x - Q.v11[0], o.y - Q.v11[1], o.z - Q.v11[2]};
-    float Pp[3] = {0.f, 0.f, 0.f};
-    Pp[J1] = dv[J2] * b2;     // cross(d, b2 e_J)
-    Pp[J2] = -(dv[J1] * b2);
-    const float detp = a2 * Pp[I];
+    const float Pp[3] = {cross_c<M21, 0>(dv, Q.e21), cross_c<M21, 1>(dv, Q.e21), cross_c<M21, 2>(dv, Q.e21)};
+    const float detp = dot_m<M23 & MPp>(Q.e23, Pp);
     const float inv_detp = rcp_det(detp);
-    const float ap = (Tp[J1] * Pp[J1] + Tp[J2] * Pp[J2]) * inv_detp;
-    float Qp[3] = {0.f, 0.f, 0.f};
-    Qp[I1] = Tp[I2] * a2;     // cross(Tp, a2 e_I)
-    Qp[I2] = -(Tp[I1] * a2);
-    const float bp = (dv[I1] * Qp[I1] + dv[I2] * Qp[I2]) * inv_detp;
+    const float Tp[3] = {o.x - Q.v11[0], o.y - Q.v11[1], o.z - Q.v11[2]};
+    const float ap = dot_m<MPp>(Tp, Pp) * inv_detp;
+    const float Qp[3] = {cross_c<M23, 0>(Tp, Q.e23), cross_c<M23, 1>(Tp, Q.e23), cross_c<M23, 2>(Tp, Q.e23)};
+    const float bp = dot_m<MQp>(dv, Qp) * inv_detp;
     ok = !(fabsf(detp) < kEps) && !(ap < 0.0f) && !(bp < 0.0f);
   }
   t_out = t;
@@ -321,13 +317,16 @@ RTP_DEV bool quad_hit_aa(const DevQuad& Q, f3 o, f3 d, float& t_out) {
 // Q.kind is wave-uniform (every lane tests the same quad): scalar branch.
 RTP_DEV bool quad_hit(const DevQuad& Q, f3 o, f3 d, float& t_out) {
   switch (Q.kind) {
-    case 1: return quad_hit_aa<0, 1>(Q, o, d, t_out);
-    case 2: return quad_hit_aa<0, 2>(Q, o, d, t_out);
-    case 3: return quad_hit_aa<1, 0>(Q, o, d, t_out);
-    case 4: return quad_hit_aa<1, 2>(Q, o, d, t_out);
-    case 5: return quad_hit_aa<2, 0>(Q, o, d, t_out);
-    case 6: return quad_hit_aa<2, 1>(Q, o, d, t_out);
-    default: return quad_hit_general(Q, o, d, t_out);
+    case 1: return quad_hit_masked<1>(Q, o, d, t_out);
+    case 2: return quad_hit_masked<2>(Q, o, d, t_out);
+    case 3: return quad_hit_masked<3>(Q, o, d, t_out);
+    case 4: return quad_hit_masked<4>(Q, o, d, t_out);
+    case 5: return quad_hit_masked<5>(Q, o, d, t_out);
+    case 6: return quad_hit_masked<6>(Q, o, d, t_out);
+    case 7: return quad_hit_masked<7>(Q, o, d, t_out);
+    case 8: return quad_hit_masked<8>(Q, o, d, t_out);
+    case 9: return quad_hit_masked<9>(Q, o, d, t_out);
+    default: return quad_hit_masked<0>(Q, o, d, t_out);
   }
 }
 

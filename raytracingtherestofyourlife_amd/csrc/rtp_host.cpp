@@ -85,22 +85,18 @@ void fill_quad(rtp::DevQuad& Q, v3 q, v3 r, v3 s, v3 t) {
   st(Q.e21, sub(r, s));
   st(Q.e23, sub(t, s));
   st(Q.n, normalize(cross(sub(r, q), sub(s, q))));  // TriangleNormal(q,r,s), Surface.h:182-183
-  // axis-aligned rectangle?  (exact zeros only; see quad_hit_aa)
-  auto axis_of = [](const float* e) -> int {
-    int nz = 0, ax = -1;
+  // zero-structure kind (exact zeros only; see quad_hit_masked)
+  auto mask_of = [](const float* e) {
+    int m = 0;
     for (int k = 0; k < 3; k++)
-      if (e[k] != 0.0f) nz++, ax = k;
-    return nz == 1 ? ax : -1;
+      if (e[k] != 0.0f) m |= 1 << k;
+    return m;
   };
-  const int I = axis_of(Q.e01), J = axis_of(Q.e03);
+  const int m01 = mask_of(Q.e01), m03 = mask_of(Q.e03), m21 = mask_of(Q.e21), m23 = mask_of(Q.e23);
   Q.kind = 0;
-  if (I >= 0 && J >= 0 && I != J && axis_of(Q.e21) == J && axis_of(Q.e23) == I) {
-    static const int kinds[3][3] = {{0, 1, 2}, {3, 0, 4}, {5, 6, 0}};
-    Q.kind = kinds[I][J];
-    Q.a = Q.e01[I];
-    Q.b = Q.e03[J];
-    Q.a2 = Q.e23[I];
-    Q.b2 = Q.e21[J];
+  for (int k = 1; k < rtp::kQuadKinds; k++) {
+    const rtp::QuadKindMasks& K = rtp::kQuadKind[k];
+    if (K.m01 == m01 && K.m03 == m03 && K.m21 == m21 && K.m23 == m23) Q.kind = k;
   }
 }
 
@@ -278,18 +274,18 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     kept.push_back(q);
     built.push_back(Q);
   }
-  // group by kind (1..6 axis-aligned, then 0 general); the device scan compares
-  // (t, orig) lexicographically, which is exactly the reference's index-order
-  // strict '<' scan, so the grouping changes no result.
+  // group by kind (scan order 1..kQuadKinds-1, then 0); the device scan
+  // compares (t, orig) lexicographically, which is exactly the reference's
+  // index-order strict '<' scan, so the grouping changes no result.
   {
-    const int order[7] = {1, 2, 3, 4, 5, 6, 0};
     int pos = 0;
-    for (int g = 0; g < 7; g++) {
+    for (int g = 0; g < rtp::kQuadKinds; g++) {
+      const int kind = (g + 1) % rtp::kQuadKinds;
       h->kind_begin[g] = pos;
       for (const rtp::DevQuad& Q : built)
-        if (Q.kind == order[g]) h->quads[pos++] = Q;
+        if (Q.kind == kind) h->quads[pos++] = Q;
     }
-    h->kind_begin[7] = pos;
+    h->kind_begin[rtp::kQuadKinds] = pos;
   }
   h->n_quads = (int32_t)kept.size();
   std::vector<rtp::DevSphere> sph(s->n_spheres);

@@ -31,6 +31,17 @@
 
 #include "rtp_device.hpp"
 
+// Cost attribution (development builds only, RTP_DUP=n): component n is
+// computed a second time on opaque copies of its inputs and its result only
+// feeds a branch that cannot be taken, so the render is unchanged and
+// T(RTP_DUP=n) - T(base) is that component's marginal cost.
+#ifndef RTP_DUP
+#define RTP_DUP 0
+#endif
+#define RTP_OPQ(x) asm volatile("" : "+v"(x))
+#define RTP_SINK(v, s) \
+  if (__float_as_uint(v) == 0x7fc12345u) (s) ^= 1u
+
 #ifndef RTP_FAIR_READY
 #define RTP_FAIR_READY 1  // pool kernel: lagging pixels jump the READY queue
 #endif
@@ -50,14 +61,15 @@ struct Hit {
 // closest-hit semantics of BVHTraverser.h:128-227 over Surface.h:208-254 /
 // 376-409 with quads visited in index order and a strict '<'.  That scan
 // returns the lexicographic minimum of (t, index) over the hits, so the quads
-// can be visited grouped by kind (one tight loop per axis-aligned orientation)
-// as long as equal t is broken by the original index.
-template <int I, int J>
-RTP_DEV void scan_aa(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d, Hit& h, int& best) {
+// can be visited grouped by zero-structure kind (one tight loop per kind) as
+// long as equal t is broken by the original index.
+template <int K>
+RTP_DEV void scan_kind(const DevScene* __restrict__ sc, int g, f3 o, f3 d, Hit& h, int& best) {
+  const int b = sc->kind_begin[g], e = sc->kind_begin[g + 1];
   for (int q = b; q < e; q++) {
     const DevQuad& Q = sc->quads[q];
     float t;
-    const bool ok = quad_hit_aa<I, J>(Q, o, d, t);
+    const bool ok = quad_hit_masked<K>(Q, o, d, t);
     const int orig = Q.orig;
     if (ok && t > 0.001f && (t < h.t || (t == h.t && orig < best))) {
       h.t = t;
@@ -136,24 +148,18 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d) {
   Hit h{3.40282347e+38f, -1, 0};
   int best = 0x7fffffff;
   const float tmin = 0.001f;
-  scan_aa<0, 1>(sc, sc->kind_begin[0], sc->kind_begin[1], o, d, h, best);
-  scan_aa<0, 2>(sc, sc->kind_begin[1], sc->kind_begin[2], o, d, h, best);
-  scan_aa<1, 0>(sc, sc->kind_begin[2], sc->kind_begin[3], o, d, h, best);
-  scan_aa<1, 2>(sc, sc->kind_begin[3], sc->kind_begin[4], o, d, h, best);
-  scan_aa<2, 0>(sc, sc->kind_begin[4], sc->kind_begin[5], o, d, h, best);
-  scan_aa<2, 1>(sc, sc->kind_begin[5], sc->kind_begin[6], o, d, h, best);
-  for (int q = sc->kind_begin[6]; q < sc->kind_begin[7]; q++) {
-    const DevQuad& Q = sc->quads[q];
-    float t;
-    const bool ok = quad_hit_general(Q, o, d, t);
-    const int orig = Q.orig;
-    if (ok && t > tmin && (t < h.t || (t == h.t && orig < best))) {
-      h.t = t;
-      h.kind = 0;
-      h.idx = q;
-      best = orig;
-    }
-  }
+  // scan order of the host's grouping: kinds 1..kQuadKinds-1, then 0
+  scan_kind<1>(sc, 0, o, d, h, best);
+  scan_kind<2>(sc, 1, o, d, h, best);
+  scan_kind<3>(sc, 2, o, d, h, best);
+  scan_kind<4>(sc, 3, o, d, h, best);
+  scan_kind<5>(sc, 4, o, d, h, best);
+  scan_kind<6>(sc, 5, o, d, h, best);
+  scan_kind<7>(sc, 6, o, d, h, best);
+  scan_kind<8>(sc, 7, o, d, h, best);
+  scan_kind<9>(sc, 8, o, d, h, best);
+  scan_kind<0>(sc, 9, o, d, h, best);
+  static_assert(kQuadKinds == 10, "closest_hit scans every kind");
   if constexpr (kBvh) {
     spheres_bvh(sc, o, d, h);
   } else {
@@ -209,6 +215,14 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
   const int d = ps.d;
   // intersect + CollectIntersecttWorklet (SurfaceWorklets.h:104-109)
   Hit h = closest_hit<kBvh>(sc, org, dir);
+#if RTP_DUP == 1
+  {
+    f3 o2 = org;
+    RTP_OPQ(o2.x);
+    const Hit h2 = closest_hit<kBvh>(sc, o2, dir);
+    RTP_SINK(h2.t, seed);
+  }
+#endif
   if (st) {
     const unsigned long long t1s = __builtin_amdgcn_s_memtime();
     dbg[kDbgCyclesIntersect] += t1s - t0;
@@ -283,6 +297,21 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
     const float rad = sqrt_exact(is_cos ? r2 : 1 - z * z);
     const float m = is_cos ? 2.0f : 1.0f;
     const f3 gcs = de_nan(local(guvw, mk(cphi * m * rad, sphi * m * rad, z)));
+#if RTP_DUP == 4
+    {
+      f3 w2 = wdir;
+      float r1b = r1;
+      RTP_OPQ(w2.x);
+      RTP_OPQ(r1b);
+      const Onb u2 = build_from_w(w2);
+      float s2, c2;
+      rtp_sincosf((float)(2 * kPi * r1b), &s2, &c2);
+      const float q2 = sqrt_exact(is_cos ? 1 - r2 : 1 - L.srr / dist2);
+      const float rad2 = sqrt_exact(is_cos ? r2 : 1 - q2 * q2);
+      const f3 g2 = de_nan(local(u2, mk(c2 * m * rad2, s2 * m * rad2, q2)));
+      RTP_SINK(g2.x, seed);
+    }
+#endif
     gen = is_quad ? genq : gcs;
 #else
     if (tw < t1) {  // cosine (PdfWorklet.h:63-79)
@@ -311,6 +340,14 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
     sum += weight * quad_pdf_value(L, hp, gen);
     (void)randf(seed);
     sum += weight * sphere_pdf_value(L, hp, gen);
+#if RTP_DUP == 2 || RTP_DUP == 3
+    {
+      f3 h2 = hp;
+      RTP_OPQ(h2.x);
+      const float v2 = RTP_DUP == 2 ? quad_pdf_value(L, h2, gen) : sphere_pdf_value(L, h2, gen);
+      RTP_SINK(v2, seed);
+    }
+#endif
     // PDFCosineWorklet (ScatterWorklet.h:96-112): mixture in double
     Onb uvw = build_from_w(hn);
     float cv;
@@ -325,6 +362,20 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
       sp = (cosine < 0) ? 0.f : cos_over_pi(cosine);
     }
     double sctr = (double)sp / pdf_val;
+#if RTP_DUP == 5
+    {
+      f3 g2 = gen;
+      RTP_OPQ(g2.x);
+      const Onb u2 = build_from_w(hn);
+      const float cs1 = dot(unit_vector(g2), u2.w);
+      const float cv2 = (cs1 > 0) ? cos_over_pi(cs1) : 0.f;
+      const double pv2 = 0.5 * (double)sum + 0.5 * (double)cv2;
+      const float cs2 = dot(hn, unit_vector(g2));
+      const float sp2 = (cs2 < 0) ? 0.f : cos_over_pi(cs2);
+      const double sc2 = (double)sp2 / pv2;
+      RTP_SINK((float)(alb.x * sc2), seed);
+    }
+#endif
     atten = mk((float)(alb.x * sctr), (float)(alb.y * sctr), (float)(alb.z * sctr));
     ps.org = hp;
     ps.dir = gen;
@@ -531,6 +582,14 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
         const bool act = mine && i < frem;
         if (!__any(act)) break;
         if (act) fseed = dead_step(fseed, t1, t2);
+#if RTP_DUP == 6
+        if (act) {
+          uint32_t f2 = fseed;
+          asm volatile("" : "+v"(f2));
+          f2 = dead_step(f2, t1, t2);
+          if (f2 == 0x12345u) fslot ^= 1;
+        }
+#endif
         iters++;
       }
       bool again = false;
@@ -578,6 +637,14 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
         const int64_t pix = pixel_of(p, (int64_t)slot * n_waves + w);
         const int pi = (int32_t)pix % p.nx, pj = (int32_t)pix / p.nx;
         ps.dir = camera_ray(p.cam, pi, pj, p.nx, p.ny, seed);
+#if RTP_DUP == 7
+        {
+          uint32_t s2 = seed;
+          asm volatile("" : "+v"(s2));
+          const f3 d2 = camera_ray(p.cam, pi, pj, p.nx, p.ny, s2);
+          RTP_SINK(d2.x, seed);
+        }
+#endif
         ps.org = eye;
         ps.d = 0;
         ps.nonfinite = false;
@@ -600,6 +667,14 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
       } else {
         const int k_end = ps.d;
         const f3 c = path_radiance(res, k_end, emit, ps.nonfinite, hist, stride);
+#if RTP_DUP == 8
+        {
+          f3 e2 = emit;
+          RTP_OPQ(e2.x);
+          const f3 c2 = path_radiance(res, k_end, e2, ps.nonfinite, hist, stride);
+          RTP_SINK(c2.x, seed);
+        }
+#endif
         s_r[slot] = s_r[slot] + c.x;  // cols += sumtotl (MapperPathTracer.cxx:350), in sample order
         s_g[slot] = s_g[slot] + c.y;
         s_b[slot] = s_b[slot] + c.z;

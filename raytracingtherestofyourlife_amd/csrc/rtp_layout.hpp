@@ -16,6 +16,21 @@ constexpr int kMaxSpheresBvh = 1 << 22;   // spheres behind the BVH (global memo
 constexpr int kBvhMinSpheres = 9;         // scenes with more spheres use the BVH
 constexpr int kBvhLeafSize = 4;
 
+// Zero-structure kinds of quads: the masks of the nonzero components of the
+// edge vectors (e01, e03, e21, e23).  A kind's test (quad_hit_masked) drops
+// every product with a structurally zero component at compile time; the host
+// assigns the kind from exact zeros.  Kind 0 is the general quad; 1..6 are
+// axis-aligned rectangles (e01 along I, e03 along J); 7..9 are the faces of
+// boxes rotated about y (edges in the xz-plane or along y).
+constexpr int kQuadKinds = 10;
+struct QuadKindMasks {
+  int m01, m03, m21, m23;
+};
+constexpr QuadKindMasks kQuadKind[kQuadKinds] = {
+    {7, 7, 7, 7},                                                               // 0 general
+    {1, 2, 2, 1}, {1, 4, 4, 1}, {2, 1, 1, 2}, {2, 4, 4, 2}, {4, 1, 1, 4}, {4, 2, 2, 4},  // 1..6 axis-aligned
+    {5, 2, 2, 5}, {2, 5, 5, 2}, {5, 5, 5, 5}};                                  // 7..9 rotated about y
+
 // One quad of the Lagae-Dutre test (Surface.h:31-161) with v00=q, v10=r,
 // v11=s, v01=t.  Read with uniform (scalar) loads.
 struct alignas(16) DevQuad {
@@ -24,12 +39,9 @@ struct alignas(16) DevQuad {
   float n[3];                    // Normalize(TriangleNormal(q,r,s)), unflipped
   float alb[3];                  // tex[texType[texIdx]]
   int32_t mt;                    // matType[matIdx]
-  // kind 0: general; 1..6: axis-aligned rectangle with e01 = a*e_I, e03 =
-  // b*e_J, e21 = b2*e_J, e23 = a2*e_I, (I,J) = (0,1),(0,2),(1,0),(1,2),(2,0),(2,1)
-  int32_t kind;
-  float a, b, a2, b2;
-  int32_t orig;  // index in the reference's quad order (tie-break of equal t)
-  int32_t pad;
+  int32_t kind;                  // index into kQuadKind
+  int32_t orig;                  // index in the reference's quad order (tie-break of equal t)
+  int32_t pad[5];
 };
 
 struct alignas(16) DevSphere {
@@ -74,14 +86,14 @@ struct alignas(16) DevLights {
 struct alignas(16) DevScene {
   int32_t n_quads;
   int32_t n_spheres;
-  // quads are stored grouped by kind: kind k occupies [kind_begin[k], kind_begin[k+1])
-  // in the order k = 1..6, then 0 (kind_begin[7] == n_quads for the general group's end)
-  int32_t kind_begin[8];
+  // quads are stored grouped by kind in the scan order 1..kQuadKinds-1, 0:
+  // group g (g-th in that order) occupies [kind_begin[g], kind_begin[g+1])
+  int32_t kind_begin[kQuadKinds + 1];
   uint32_t which_t1;  // smallest hash with which >= 2   (PdfWorklet.h:20)
   uint32_t which_t2;  // smallest hash with which == 3
   float ior;
   int32_t n_nodes;                 // BVH scenes (n_spheres >= kBvhMinSpheres)
-  int32_t pad[2];
+  int32_t pad[3];
   const BvhNode* nodes;
   const DevSphereG* sph_geom;      // BVH leaf order
   const DevSphere* sph_all;        // scene order (materials of the hit sphere)
