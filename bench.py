@@ -102,6 +102,10 @@ def main() -> None:
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work (0: skip)")
     ap.add_argument("--cpu-budget-mt", type=float, default=6.0, help="seconds of all-cores CPU baseline (0: skip)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (RCCL over xGMI, production); gloo: host-side reduce, for rehearsing N>1 on one GPU")
+    ap.add_argument("--share-gpu", action="store_true", help="every rank uses device 0 (rehearsal on a 1-GPU box)")
+    ap.add_argument("--check", action="store_true", help="rank 0 verifies the reduced canvas against a 1-process render")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c2.json"))
     args = ap.parse_args()
 
@@ -116,14 +120,18 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
+    gpu = 0 if args.share_gpu else local
+    torch.cuda.set_device(gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
 
     nx, ny = args.nx, args.ny * world
     ids_np = shard.tile_pixels(nx, ny, rank, world)
     npix = ids_np.size
-    dev = rtp.Device(local)
+    dev = rtp.Device(gpu)
     dev.set_cornell_box(0)
     cam = rtp.default_camera()
     ids = torch.from_numpy(ids_np).cuda()
@@ -132,14 +140,24 @@ def main() -> None:
     live = torch.zeros(npix, dtype=torch.int32, device="cuda")
     stream = torch.cuda.current_stream()
 
+    def reduce_canvas():
+        if world == 1:
+            return
+        if args.dist_backend == "nccl":
+            dist.reduce(canvas, dst=0, op=dist.ReduceOp.SUM)
+        else:  # gloo reduces host tensors
+            host = canvas.cpu()
+            dist.reduce(host, dst=0, op=dist.ReduceOp.SUM)
+            if rank == 0:
+                canvas.copy_(host)
+
     def step(count_live: bool = False):
         dev.render_device(cam, nx, ny, args.spp, args.depth, out.data_ptr(), pixel_count=npix,
                           pixel_ids_ptr=ids.data_ptr(), stream=stream.cuda_stream,
                           live_ptr=live.data_ptr() if count_live else 0)
         canvas.zero_()
         canvas.index_copy_(0, ids, out)
-        if world > 1:
-            dist.reduce(canvas, dst=0, op=dist.ReduceOp.SUM)
+        reduce_canvas()
 
     for i in range(args.warmup):
         step(count_live=(i == 0))
@@ -161,15 +179,24 @@ def main() -> None:
         ev[k][1].record(stream)
         canvas.zero_()
         canvas.index_copy_(0, ids, out)
-        if world > 1:
-            dist.reduce(canvas, dst=0, op=dist.ReduceOp.SUM)
+        reduce_canvas()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if args.steps else float("nan")
+    check = None
+    if args.check and rank == 0:
+        # the reduced canvas must equal one process rendering every pixel (bit-exact, NaN-aware)
+        full = torch.empty((nx * ny, 4), dtype=torch.float32, device="cuda")
+        dev.render_device(cam, nx, ny, args.spp, args.depth, full.data_ptr(), stream=stream.cuda_stream)
+        torch.cuda.synchronize()
+        a, b = canvas[:, :3].cpu().numpy(), full[:, :3].cpu().numpy()
+        same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+        check = bool(same.all())
     if world > 1:
-        t = torch.tensor([elapsed, live_total], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, live_total], dtype=torch.float64,
+                         device="cuda" if args.dist_backend == "nccl" else "cpu")
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         tot = t.clone()
@@ -227,6 +254,8 @@ def main() -> None:
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_mt,
         }
+        if check is not None:
+            line["check_reduced_canvas_equals_single_render"] = check
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
