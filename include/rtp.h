@@ -146,7 +146,9 @@ rtp_status rtp_cornell_box(int32_t variant, rtp_scene_desc* out);
 
 /* Diagnostics: evaluate a device primitive elementwise (tests only).
  * kind 0: glibc-exact sinf port, 1: cosf port, 2: 1/sqrtf(x) (RMagnitude),
- * 3: wang32 (bit pattern in/out).  in/out: n 4-byte elements, host memory. */
+ * 3: wang32 (bit pattern in/out), 4 / 5: the RNG jump tables (state after
+ * 16 / 32 dead depths; RTP_ERR_DEVICE if they are not built), 6: the state
+ * after one dead depth.  in/out: n 4-byte elements, host memory. */
 rtp_status rtp_eval_primitive(rtp_context* ctx, int32_t kind, const void* in, void* out, int64_t n);
 
 /* Diagnostics: with RTP_DEBUG_STATS=1 in the environment the render kernel

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -22,7 +23,9 @@
 extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int bvh, int* variant_out, int* waves_out);
 extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::KParams* p, int variant, int waves, int bvh,
                                         hipStream_t stream);
-extern "C" hipError_t rtp_launch_eval_primitive(int kind, const void* in, void* out, int64_t n, hipStream_t stream);
+extern "C" hipError_t rtp_launch_eval_primitive(int kind, const void* in, void* out, int64_t n, const uint32_t* tab,
+                                                uint32_t t1, uint32_t t2, hipStream_t stream);
+extern "C" hipError_t rtp_launch_build_ff_table(uint32_t* T, int steps, uint32_t t1, uint32_t t2, hipStream_t stream);
 extern "C" hipError_t rtp_launch_verify_fast_math(int kind, uint32_t lo, uint64_t count, unsigned long long* bad,
                                                   uint32_t* first_bad, hipStream_t stream);
 
@@ -101,6 +104,62 @@ void fill_quad(rtp::DevQuad& Q, v3 q, v3 r, v3 s, v3 t) {
 }
 
 bool bit_equal(const float* a, const float* b, int n) { return std::memcmp(a, b, sizeof(float) * n) == 0; }
+
+// RNG jump tables.  A dead depth consumes 1 + {2,3,2} draws chosen by the
+// `which` draw against two constant thresholds (lightables = 2,
+// MapperPathTracer.cxx:218; PdfWorklet.h:20), so "advance the state over k
+// dead depths" is a fixed map of the 32-bit state.  Table j tabulates it for
+// k = 32 >> j over all 2^32 states (16 GiB each; built once per device and
+// process, shared by every context).  The pool kernel's fast-forward then
+// takes a few table reads instead of ~150 hashes per sample.  RTP_FF_TABLES=n
+// (0..4, default 2: 32 GiB) sets how many tables (32, 16, 8, 4 depths) to build;
+// fewer are built when the device lacks the memory (8 GiB kept free).
+struct FfTables {
+  uint32_t* t[rtp::kFfTables] = {};
+  bool tried = false;
+  float build_ms = 0.f;
+};
+std::mutex g_ff_mu;
+FfTables g_ff[64];
+
+const FfTables& ff_tables(int device) {
+  std::lock_guard<std::mutex> lk(g_ff_mu);
+  FfTables& T = g_ff[device & 63];
+  if (T.tried) return T;
+  T.tried = true;
+  int want = 2;
+  if (const char* env = getenv("RTP_FF_TABLES")) want = std::max(0, std::min(rtp::kFfTables, atoi(env)));
+  const size_t bytes = (size_t)4 << 32;
+  const uint32_t t1 = which_threshold(2), t2 = which_threshold(3);
+  hipEvent_t a = nullptr, b = nullptr;
+  if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return T;
+  (void)hipEventRecord(a, nullptr);
+  for (int j = 0; j < want; j++) {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < bytes + (8ull << 30)) break;
+    if (hipMalloc(&T.t[j], bytes) != hipSuccess) {
+      T.t[j] = nullptr;
+      break;
+    }
+    if (rtp_launch_build_ff_table(T.t[j], 32 >> j, t1, t2, nullptr) != hipSuccess) {
+      (void)hipFree(T.t[j]);
+      T.t[j] = nullptr;
+      break;
+    }
+  }
+  (void)hipEventRecord(b, nullptr);
+  if (hipEventSynchronize(b) != hipSuccess) {
+    for (uint32_t*& p : T.t) {
+      if (p) (void)hipFree(p);
+      p = nullptr;
+    }
+  }
+  (void)hipEventElapsedTime(&T.build_ms, a, b);
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  (void)hipGetLastError();
+  return T;
+}
 
 // Sphere BVH (replaces the VTK-m LinearBVH of buildBVH, MapperPathTracer.cxx:
 // 437-449, for scenes with many spheres).  Median split on the longest axis
@@ -461,6 +520,10 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
   p.hist = c->d_hist;
   p.dbg = nullptr;
   p.progress = c->d_progress;
+  if (variant == 2) {
+    const FfTables& ft = ff_tables(c->device);
+    for (int j = 0; j < rtp::kFfTables; j++) p.ff[j] = ft.t[j];
+  }
   HIP_TRY(hipMemsetAsync(c->d_progress, 0, 8, stream));
   {
     const char* e = getenv("RTP_DEBUG_STATS");
@@ -617,18 +680,25 @@ int32_t rtp_debug_counters(rtp_context* c, uint64_t* out, int32_t n_out) {
 }
 
 rtp_status rtp_eval_primitive(rtp_context* c, int32_t kind, const void* in, void* out, int64_t n) {
-  if (!c || !in || !out || n < 0 || kind < 0 || kind > 3)
+  if (!c || !in || !out || n < 0 || kind < 0 || kind > 6)
     return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_eval_primitive: bad arguments");
   if (n == 0) return RTP_OK;
   HIP_TRY(hipSetDevice(c->device));
+  const uint32_t* tab = nullptr;
+  if (kind == 4 || kind == 5) {
+    const FfTables& ft = ff_tables(c->device);
+    tab = kind == 4 ? ft.t[1] : ft.t[0];  // 16 / 32 dead depths
+    if (!tab) return fail(RTP_ERR_DEVICE, "rtp_eval_primitive: RNG jump tables are not built (RTP_FF_TABLE=0 or memory)");
+  }
+  const int dk = kind <= 3 ? kind : (kind <= 5 ? 4 : 5);  // device kinds: 4 gather, 5 one dead step
   void *din = nullptr, *dout = nullptr;
   HIP_TRY(hipMalloc(&din, (size_t)n * 4));
   hipError_t e = hipMalloc(&dout, (size_t)n * 4);
   if (e == hipSuccess) e = hipMemcpy(din, in, (size_t)n * 4, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = rtp_launch_eval_primitive(kind, din, dout, n, nullptr);
+  if (e == hipSuccess) e = rtp_launch_eval_primitive(dk, din, dout, n, tab, which_threshold(2), which_threshold(3), nullptr);
   if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)n * 4, hipMemcpyDeviceToHost);
-  hipFree(din);
-  if (dout) hipFree(dout);
+  (void)hipFree(din);
+  if (dout) (void)hipFree(dout);
   if (e != hipSuccess) return hip_fail(e, "rtp_eval_primitive");
   return RTP_OK;
 }

@@ -577,6 +577,17 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
         fseed = s_seed[fslot];
         frem = s_rem[fslot];
       }
+      // jump over 32 / 16 / 8 / 4 dead depths with one table read each
+      // (HBM-resident tables of the dead-step map, built once per device),
+      // then hash the few remaining depths
+#pragma unroll
+      for (int j = 0; j < kFfTables; j++) {
+        const uint32_t* __restrict__ tab = p.ff[j];
+        if (tab != nullptr && mine && frem >= (32 >> j)) {
+          fseed = tab[fseed];
+          frem -= 32 >> j;
+        }
+      }
       int iters = 0;
       for (int i = 0;; i++) {
         const bool act = mine && i < frem;
@@ -734,7 +745,8 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
 }
 
 // ------------------------------------------------------- diagnostics ---
-__global__ void rtp_eval_primitive_kernel(int kind, const void* in, void* out, int64_t n) {
+__global__ void rtp_eval_primitive_kernel(int kind, const void* in, void* out, int64_t n, const uint32_t* tab,
+                                          uint32_t t1, uint32_t t2) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float* fi = static_cast<const float*>(in);
@@ -746,8 +758,20 @@ __global__ void rtp_eval_primitive_kernel(int kind, const void* in, void* out, i
     case 1: fo[i] = rtp_cosf(fi[i]); break;
     case 2: fo[i] = 1.0f / __builtin_sqrtf(fi[i]); break;
     case 3: uo[i] = wang(ui[i]); break;
+    case 4: uo[i] = tab[ui[i]]; break;          // jump-table gather (ff16 / ff32)
+    case 5: uo[i] = dead_step(ui[i], t1, t2); break;
     default: break;
   }
+}
+
+// Dead-step jump table: T[s] = dead_step^steps(s) for s in [base, base+count).
+__global__ void rtp_build_ff_table_kernel(uint32_t* __restrict__ T, int steps, uint32_t t1, uint32_t t2, uint64_t base,
+                                          uint64_t count) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  uint32_t s = (uint32_t)(base + i);
+  for (int k = 0; k < steps; k++) s = dead_step(s, t1, t2);
+  T[base + i] = s;
 }
 
 // Exhaustive equivalence check of a fast sequence against the IEEE operation
@@ -856,10 +880,23 @@ extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::K
   return hipGetLastError();
 }
 
-extern "C" hipError_t rtp_launch_eval_primitive(int kind, const void* in, void* out, int64_t n, hipStream_t stream) {
+extern "C" hipError_t rtp_launch_build_ff_table(uint32_t* T, int steps, uint32_t t1, uint32_t t2, hipStream_t stream) {
+  const uint64_t total = 1ull << 32, chunk = 1ull << 30;
+  for (uint64_t base = 0; base < total; base += chunk) {
+    hipLaunchKernelGGL(rtp::rtp_build_ff_table_kernel, dim3((unsigned)(chunk / 256)), dim3(256), 0, stream, T, steps,
+                       t1, t2, base, chunk);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+extern "C" hipError_t rtp_launch_eval_primitive(int kind, const void* in, void* out, int64_t n, const uint32_t* tab,
+                                                uint32_t t1, uint32_t t2, hipStream_t stream) {
   const int block = 256;
   const int64_t grid = (n + block - 1) / block;
   if (grid <= 0) return hipSuccess;
-  hipLaunchKernelGGL(rtp::rtp_eval_primitive_kernel, dim3((unsigned)grid), dim3(block), 0, stream, kind, in, out, n);
+  hipLaunchKernelGGL(rtp::rtp_eval_primitive_kernel, dim3((unsigned)grid), dim3(block), 0, stream, kind, in, out, n,
+                     tab, t1, t2);
   return hipGetLastError();
 }

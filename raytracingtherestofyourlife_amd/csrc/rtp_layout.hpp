@@ -107,6 +107,8 @@ struct DevCamera {
   float eye[3], nlook[3], dx[3], dy[3];
 };
 
+constexpr int kFfTables = 4;  // jump tables for 32, 16, 8, 4 dead depths
+
 struct KParams {
   DevCamera cam;
   int32_t nx, ny, spp, depth;
@@ -120,6 +122,9 @@ struct KParams {
   float* hist;               // float4[(depth-1) * lanes] attenuation history, depth-major
   unsigned long long* dbg;   // nullable: per-wave counters (kDbgCounters each), diagnostics only
   unsigned long long* progress;  // zeroed before launch: samples finished by all waves (issue-priority balancing)
+  // RNG jump tables (nullable): ff[j][s] = the state after (32 >> j) dead
+  // depths from state s (2^32 entries each, 16 GiB; rtp_host.cpp)
+  const uint32_t* ff[kFfTables];
 };
 
 // per-wave diagnostic counters of the pool kernel (RTP_DEBUG_STATS=1)
