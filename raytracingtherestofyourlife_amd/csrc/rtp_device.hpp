@@ -301,6 +301,19 @@ RTP_DEV bool quad_hit_masked(const DevQuad& Q, f3 o, f3 d, float& t_out) {
   const float t = dot_m<M03 & MQ>(Q.e03, Qv) * inv_det;
   bool ok = !(fabsf(det) < kEps) && !(alpha < 0.0f) && !(beta < 0.0f) && !(t < 0.0f);
   if (ok && (alpha + beta) > 1.0f) {
+    if (Q.para) {
+      // exact parallelogram: e21 == -e03 and e23 == -e01 bit for bit, so
+      // Pp == -P, detp == det (the same products with both factors negated),
+      // Qp == -cross(Tp, e01); negation commutes with rounding.
+      static_assert(M21 == M03 && M23 == M01, "kinds pair e21 with e03 and e23 with e01");
+      const float Tp[3] = {o.x - Q.v11[0], o.y - Q.v11[1], o.z - Q.v11[2]};
+      const float ap = -dot_m<MP>(Tp, P) * inv_det;
+      const float Qp[3] = {cross_c<M01, 0>(Tp, Q.e01), cross_c<M01, 1>(Tp, Q.e01), cross_c<M01, 2>(Tp, Q.e01)};
+      const float bp = -dot_m<MQ>(dv, Qp) * inv_det;
+      ok = !(ap < 0.0f) && !(bp < 0.0f);
+      t_out = t;
+      return ok;
+    }
     const float Pp[3] = {cross_c<M21, 0>(dv, Q.e21), cross_c<M21, 1>(dv, Q.e21), cross_c<M21, 2>(dv, Q.e21)};
     const float detp = dot_m<M23 & MPp>(Q.e23, Pp);
     const float inv_detp = rcp_det(detp);

@@ -96,6 +96,11 @@ void fill_quad(rtp::DevQuad& Q, v3 q, v3 r, v3 s, v3 t) {
     return m;
   };
   const int m01 = mask_of(Q.e01), m03 = mask_of(Q.e03), m21 = mask_of(Q.e21), m23 = mask_of(Q.e23);
+  // exact parallelogram (see quad_hit_masked): value equality; the sign of a
+  // zero component only ever changes the sign of a zero intermediate
+  Q.para = 1;
+  for (int k = 0; k < 3; k++)
+    if (!(-Q.e01[k] == Q.e23[k] && -Q.e03[k] == Q.e21[k])) Q.para = 0;
   Q.kind = 0;
   for (int k = 1; k < rtp::kQuadKinds; k++) {
     const rtp::QuadKindMasks& K = rtp::kQuadKind[k];
