@@ -35,9 +35,11 @@ def test_shim_check(programs, tmp_path):
 
 
 def test_driver_out_of_scope_modes(programs):
-    for flag in ("-hemisphere", "-direct"):
-        r = subprocess.run([programs["rtp_path"], flag], capture_output=True, text=True, timeout=60)
-        assert r.returncode == 2 and "out of scope" in r.stderr
+    r = subprocess.run([programs["rtp_path"], "-direct"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "out of scope" in r.stderr
+    r = subprocess.run([programs["rtp_path"], "-hemisphere", "-rank", "3", "-world", "2"], capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode == 2
 
 
 @pytest.mark.skipif(not _no_hip_device(), reason="a HIP device is present")
@@ -76,3 +78,77 @@ def test_driver_c1_matches_golden(programs, oracle, tmp_path):
     want = oracle.normalize(want, spp)
     assert np.array_equal(got[:, :3].view(np.uint32), want[:, :3].view(np.uint32))
     assert (tmp_path / "output.pnm").read_bytes() == _pnm_bytes(want[:, :3], nx, ny)
+
+
+def _hemisphere_plan_py(phi_count, theta_count):
+    """generateHemisphere's views (main.cc:504-561, parameters from :583-595)
+    restated with numpy float32 and glibc's cosf/sinf (the float overloads)."""
+    import ctypes
+
+    libm = ctypes.CDLL("libm.so.6")
+    for fn in ("cosf", "sinf"):
+        getattr(libm, fn).restype = ctypes.c_float
+        getattr(libm, fn).argtypes = [ctypes.c_float]
+    f32 = np.float32
+    phi_end, theta_end = f32(1.0), f32(2 * 3.14159265358979323846)
+    r_theta = f32(theta_end / f32(theta_count))
+    r_phi = f32((phi_end - f32(0.0)) / f32(phi_count))
+    r = f32(-1078 / 555.0)
+    views = []
+    phi = f32(0.0)
+    while float(phi) < float(phi_end) - 0.5 * float(r_phi):
+        theta = f32(0.0)
+        while theta < theta_end:
+            c, s = f32(libm.cosf(float(theta))), f32(libm.sinf(float(theta)))
+            sp, cp = f32(libm.sinf(float(phi))), f32(libm.cosf(float(phi)))
+            p = [f32(f32(r * c) * sp), f32(f32(r * s) * sp), f32(r * cp)]
+            pos = [f32(float(v) + 278 / 555.0) for v in p]
+            views.append(("%.4f-%.4f" % (phi, theta), [int(np.array(v, np.float32).view(np.uint32)) for v in pos]))
+            theta = f32(theta + r_theta)
+        phi = f32(phi + r_phi)
+    return views
+
+
+def _dry_run(programs, *args):
+    r = subprocess.run([programs["rtp_path"], "-hemisphere", "-dry-run", *args], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 0, r.stderr
+    out = []
+    for line in r.stdout.split("\n"):
+        if line.strip():
+            name, *hx = line.split()
+            out.append((name, [int(h, 16) for h in hx]))
+    return out
+
+
+@pytest.mark.parametrize("pc,tc", [(15, 15), (3, 4), (7, 5)])
+def test_hemisphere_views_match_restatement(programs, pc, tc):
+    got = _dry_run(programs, "-phicount", str(pc), "-thetacount", str(tc))
+    assert got == _hemisphere_plan_py(pc, tc)
+
+
+def test_hemisphere_view_sharding(programs):
+    full = _dry_run(programs, "-phicount", "4", "-thetacount", "5")
+    parts = [_dry_run(programs, "-phicount", "4", "-thetacount", "5", "-rank", str(k), "-world", "3") for k in range(3)]
+    assert [v for k in range(3) for v in parts[k]] != [] and sorted(sum(parts, [])) == sorted(full)
+    assert parts[1] == full[1::3]
+
+
+@pytest.mark.gpu
+def test_hemisphere_views_render_like_oracle(programs, oracle, tmp_path):
+    nx, ny, spp, depth = 24, 16, 3, 6
+    r = subprocess.run([programs["rtp_path"], "-hemisphere", "-phicount", "2", "-thetacount", "2", "-x", str(nx), "-y",
+                        str(ny), "-samplecount", str(spp), "-raydepth", str(depth), "-o", str(tmp_path / "output"),
+                        "-raw", str(tmp_path / "raw")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    views = _hemisphere_plan_py(2, 2)
+    assert len(views) == 4
+    sc = oracle.cornell_box(0)
+    for name, pos_bits in views:
+        pos = np.array(pos_bits, dtype=np.uint32).view(np.float32)
+        cam = oracle.camera_setup(nx, ny, position=pos)
+        want, _, _ = oracle.render_pixels(sc, cam, nx, ny, spp, depth, np.arange(nx * ny, dtype=np.int64))
+        want = oracle.normalize(want, spp)
+        got = np.fromfile(tmp_path / f"raw-{name}.f32", dtype=np.float32).reshape(nx * ny, 4)
+        assert np.array_equal(got[:, :3].view(np.uint32), want[:, :3].view(np.uint32)), name
+        assert (tmp_path / f"output-{name}.pnm").read_bytes() == _pnm_bytes(want[:, :3], nx, ny)
