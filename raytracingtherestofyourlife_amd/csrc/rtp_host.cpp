@@ -519,7 +519,7 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
   p.live_out = d_live;
   int variant = 2, waves = 0;
   const int64_t lanes = rtp_plan_history_lanes(npix, c->use_bvh ? 1 : 0, &variant, &waves);
-  size_t hist_need = (size_t)(depth > 1 ? depth - 1 : 1) * (size_t)lanes * 16;
+  size_t hist_need = (size_t)depth * (size_t)lanes * 16;  // D rows (row k of a light hit holds E_k)
   rtp_status rs = ensure_hist(c, hist_need);
   if (rs != RTP_OK) return rs;
   p.hist = c->d_hist;

@@ -45,6 +45,9 @@
 #ifndef RTP_FAIR_READY
 #define RTP_FAIR_READY 1  // pool kernel: lagging pixels jump the READY queue
 #endif
+#ifndef RTP_DEFER_RADIANCE
+#define RTP_DEFER_RADIANCE 1  // pool kernel: radiance product in the fast-forward batch
+#endif
 #ifndef RTP_MERGED_GEN
 #define RTP_MERGED_GEN 1  // branch-free generator pass (bounce); 0: the three divergent branches
 #endif
@@ -459,6 +462,8 @@ constexpr int kWavesPerBlock = 4;
 constexpr int kPool = 256;  // pixel slots per wave (power of two: queue index = cursor & (kPool-1))
 // LDS per wave: seed, r, g, b, samples, live (u32) + rem, q_ready, q_ff, pad (u16)
 constexpr int kSlotBytes = 6 * 4 + 4 * 2;
+// s_rem packs the remaining dead depths with how the sample's path ended
+constexpr int kRemMask = 0x3fff, kEndLight = 0x4000, kEndNonfinite = 0x8000;
 constexpr int kPoolLdsBytes = kWavesPerBlock * kPool * kSlotBytes;
 
 RTP_DEV uint32_t lane_rank(uint64_t mask) {  // number of set mask bits below this lane
@@ -533,8 +538,18 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
   int unfinished = n_slots;                // stats only: pixels with samples still to run
   unsigned long long t_tail = 0;
 
+#if RTP_DEFER_RADIANCE
+  // attenuation history per pixel SLOT, [d][wave*kPool + slot], D rows: a
+  // pixel has one sample in flight, so its history survives until the
+  // fast-forward batch that computes the sample's radiance (row k of a
+  // light hit holds E_k)
+  float4* __restrict__ const hist_base = reinterpret_cast<float4*>(p.hist) + (int64_t)w * kPool;
+  const int64_t stride = (int64_t)n_waves * kPool;
+  float4* __restrict__ hist = hist_base;  // per lane: hist_base + slot of its path
+#else
   float4* __restrict__ hist = reinterpret_cast<float4*>(p.hist) + ((int64_t)w * 64 + lane);  // [d][lane]
   const int64_t stride = (int64_t)n_waves * 64;
+#endif
   const f3 eye = ld3(p.cam.eye);
 
   // diagnostics (uniform branch on a kernel argument; off in production)
@@ -577,6 +592,34 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
         fseed = s_seed[fslot];
         frem = s_rem[fslot];
       }
+#if RTP_DEFER_RADIANCE
+      if (mine) {
+        // back-to-front radiance of the pixel's finished sample (path_radiance),
+        // banked in sample order before the pixel's next sample can start
+        const int flags = frem;
+        frem &= kRemMask;
+        f3 c;
+        if (flags & kEndLight) {
+          const int k_end = D - 1 - frem;
+          const float4* __restrict__ hp = hist_base + fslot;
+          const float4 e = hp[(int64_t)k_end * stride];
+          float sx = e.x + 0.0f, sy = e.y + 0.0f, sz = e.z + 0.0f;
+          for (int dd = k_end - 1; dd >= 0; dd--) {
+            const float4 a = hp[(int64_t)dd * stride];
+            sx = 0.0f + a.x * sx;
+            sy = 0.0f + a.y * sy;
+            sz = 0.0f + a.z * sz;
+          }
+          c = mk(sx, sy, sz);
+        } else {
+          const float v = (flags & kEndNonfinite) ? __builtin_nanf("") : 0.0f;
+          c = mk(v, v, v);
+        }
+        s_r[fslot] = s_r[fslot] + c.x;  // cols += sumtotl (MapperPathTracer.cxx:350), in sample order
+        s_g[fslot] = s_g[fslot] + c.y;
+        s_b[fslot] = s_b[fslot] + c.z;
+      }
+#endif
       // jump over 32 / 16 / 8 / 4 dead depths with one table read each
       // (HBM-resident tables of the dead-step map, built once per device),
       // then hash the few remaining depths
@@ -645,6 +688,9 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
       if (r < take) {
         slot = q_ready[(ready_head + r) & (kPool - 1)];
         seed = s_seed[slot];
+#if RTP_DEFER_RADIANCE
+        hist = hist_base + slot;
+#endif
         const int64_t pix = pixel_of(p, (int64_t)slot * n_waves + w);
         const int pi = (int32_t)pix % p.nx, pj = (int32_t)pix / p.nx;
         ps.dir = camera_ray(p.cam, pi, pj, p.nx, p.ny, seed);
@@ -677,22 +723,21 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
         ps.d++;
       } else {
         const int k_end = ps.d;
+#if RTP_DEFER_RADIANCE
+        // the radiance product runs in the fast-forward batch (above)
+        if (res == kLight) hist[(int64_t)k_end * stride] = make_float4(emit.x, emit.y, emit.z, 0.f);
+        s_rem[slot] = (uint16_t)((D - 1 - k_end) | (res == kLight ? kEndLight : 0) |
+                                 (ps.nonfinite ? kEndNonfinite : 0));
+#else
         const f3 c = path_radiance(res, k_end, emit, ps.nonfinite, hist, stride);
-#if RTP_DUP == 8
-        {
-          f3 e2 = emit;
-          RTP_OPQ(e2.x);
-          const f3 c2 = path_radiance(res, k_end, e2, ps.nonfinite, hist, stride);
-          RTP_SINK(c2.x, seed);
-        }
-#endif
         s_r[slot] = s_r[slot] + c.x;  // cols += sumtotl (MapperPathTracer.cxx:350), in sample order
         s_g[slot] = s_g[slot] + c.y;
         s_b[slot] = s_b[slot] + c.z;
+        s_rem[slot] = (uint16_t)(D - 1 - k_end);
+#endif
         s_samples[slot] = s_samples[slot] + 1u;
         s_live[slot] = s_live[slot] + (uint32_t)(k_end + 1);
         s_seed[slot] = seed;
-        s_rem[slot] = (uint16_t)(D - 1 - k_end);
         ended = true;
         has_path = false;
       }
@@ -855,7 +900,7 @@ extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int bvh, int* variant_ou
   W = std::max<int64_t>(W, by_pool);
   W = std::max<int64_t>(W, 1);
   if (waves_out) *waves_out = (int)W;
-  return W * 64;
+  return RTP_DEFER_RADIANCE ? W * rtp::kPool : W * 64;
 }
 
 extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::KParams* p, int variant, int waves,
