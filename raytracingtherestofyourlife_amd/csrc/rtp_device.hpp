@@ -394,11 +394,11 @@ RTP_DEV f3 random_to_sphere(float rr, float dist2, float r1, float r2) {  // Pdf
 
 // QuadPDFWorklet::pdf_value (PdfWorklet.h:230-248).  The normal flip of
 // intersect() is dropped: fabs(dot(v,-n)*k) == fabs(dot(v,n)*k) exactly.
-RTP_DEV float quad_pdf_value(const DevLights& L, f3 o, f3 v) {
+RTP_DEV float quad_pdf_value(const DevLights& L, f3 o, f3 v, float rmag_v) {  // rmag_v == rmag(v)
   float t;
   if (quad_hit(L.quad, o, v, t) && t < 3.40282347e+38f && t > 0.001f) {
     float distance_squared = t * t * dot(v, v);
-    float cosine = fabsf(dot(v, ld3(L.quad.n)) * rmag(v));
+    float cosine = fabsf(dot(v, ld3(L.quad.n)) * rmag_v);
     return distance_squared / (cosine * L.area);
   }
   return 0;
@@ -427,18 +427,19 @@ RTP_DEV void dielectric_scatter(f3 dir, f3 n, float ref_idx, float rnd, f3& sd) 
   f3 refracted = mk(0, 0, 0);  // reference reads an uninitialised vec3 here when refraction fails and rnd==1
   f3 outward;
   float ni_over_nt, cosine;
+  const float rm = rmag(dir);  // one 1/|dir| for the cosine and unit_vector(dir)
   if (dot(dir, n) > 0) {
     outward = neg(n);
     ni_over_nt = ref_idx;
-    cosine = ref_idx * dot(dir, n) * rmag(dir);
+    cosine = ref_idx * dot(dir, n) * rm;
   } else {
     outward = n;
     ni_over_nt = (float)(1.0 / ref_idx);
-    cosine = -dot(dir, n) * rmag(dir);
+    cosine = -dot(dir, n) * rm;
   }
   float reflect_prob;
   {  // refract (EmitWorklet.h:160-170)
-    f3 uv = unit_vector(dir);
+    f3 uv = scl(dir, rm);
     float dt = dot(uv, outward);
     float discriminant = (float)(1.0 - ni_over_nt * ni_over_nt * (1 - dt * dt));
     if (discriminant > 0) {

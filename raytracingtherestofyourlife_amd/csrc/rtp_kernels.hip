@@ -207,7 +207,10 @@ enum BounceResult { kAlive = 0, kMissed = 1, kLight = 2 };
 // (when d <= D-2).  On kLight, `emit` receives E[d].
 RTP_DEV unsigned long long stamp(bool on) { return on ? __builtin_amdgcn_s_memtime() : 0ull; }
 
-template <bool kBvh>
+// kDeferDead: a path that misses or hits the light at depth k leaves its
+// depth-k draws (which + generator, exactly one dead step) to the caller's
+// fast-forward instead of drawing them here.
+template <bool kBvh, bool kDeferDead = false>
 RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3& emit, float4* __restrict__ hist_d,
                    int D, unsigned long long* dbg = nullptr) {
   const bool st = dbg != nullptr;
@@ -231,7 +234,7 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
     dbg[kDbgCyclesIntersect] += t1s - t0;
   }
   if (h.kind < 0) {
-    seed = dead_step(seed, t1, t2);  // which + generator draws of the now-dead ray
+    if (!kDeferDead) seed = dead_step(seed, t1, t2);  // which + generator draws of the now-dead ray
     return kMissed;
   }
   f3 hp = add(org, scl(dir, h.t));
@@ -253,7 +256,7 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
   // applyMaterials (EmitWorklet.h)
   if (mt == 1) {  // DiffuseLightWorklet: emit, path ends (status &= 0)
     emit = (dot(hn, dir) < 0.0f) ? alb : mk(0.f, 0.f, 0.f);
-    seed = dead_step(seed, t1, t2);
+    if (!kDeferDead) seed = dead_step(seed, t1, t2);
     return kLight;
   }
   f3 atten;
@@ -340,28 +343,31 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
     // applyPDFs: QuadPDFWorklet, SpherePDFWorklet (1 discarded draw)
     const float weight = 0.5f;
     float sum = 0;
-    sum += weight * quad_pdf_value(L, hp, gen);
+    // 1/|gen| once: QuadPDFWorklet's rmag and both unit_vector(gen) below
+    const float rg = rmag(gen);
+    sum += weight * quad_pdf_value(L, hp, gen, rg);
     (void)randf(seed);
     sum += weight * sphere_pdf_value(L, hp, gen);
 #if RTP_DUP == 2 || RTP_DUP == 3
     {
       f3 h2 = hp;
       RTP_OPQ(h2.x);
-      const float v2 = RTP_DUP == 2 ? quad_pdf_value(L, h2, gen) : sphere_pdf_value(L, h2, gen);
+      const float v2 = RTP_DUP == 2 ? quad_pdf_value(L, h2, gen, rmag(gen)) : sphere_pdf_value(L, h2, gen);
       RTP_SINK(v2, seed);
     }
 #endif
     // PDFCosineWorklet (ScatterWorklet.h:96-112): mixture in double
-    Onb uvw = build_from_w(hn);
+    const f3 ug = scl(gen, rg);       // unit_vector(gen)
+    const f3 w_hn = unit_vector(hn);  // build_from_w(hn).w (u and v are unused here)
     float cv;
     {
-      float cosine = dot(unit_vector(gen), uvw.w);
+      float cosine = dot(ug, w_hn);
       cv = (cosine > 0) ? cos_over_pi(cosine) : 0.f;
     }
     double pdf_val = 0.5 * (double)sum + 0.5 * (double)cv;
     float sp;
     {
-      float cosine = dot(hn, unit_vector(gen));
+      float cosine = dot(hn, ug);
       sp = (cosine < 0) ? 0.f : cos_over_pi(cosine);
     }
     double sctr = (double)sp / pdf_val;
@@ -600,7 +606,7 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
         frem &= kRemMask;
         f3 c;
         if (flags & kEndLight) {
-          const int k_end = D - 1 - frem;
+          const int k_end = D - frem;  // a light hit ends the path: rem = D - 1 - k_end + 1
           const float4* __restrict__ hp = hist_base + fslot;
           const float4 e = hp[(int64_t)k_end * stride];
           float sx = e.x + 0.0f, sy = e.y + 0.0f, sz = e.z + 0.0f;
@@ -717,7 +723,7 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
     unsigned long long tbnc = ta;
     if (has_path) {
       f3 emit = mk(0.f, 0.f, 0.f);
-      const int res = bounce<kBvh>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D, want_dbg ? dbg : nullptr);
+      const int res = bounce<kBvh, true>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D, want_dbg ? dbg : nullptr);
       tbnc = stamp(want_dbg);
       if (res == kAlive && ps.d < D - 1) {
         ps.d++;
@@ -726,14 +732,16 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
 #if RTP_DEFER_RADIANCE
         // the radiance product runs in the fast-forward batch (above)
         if (res == kLight) hist[(int64_t)k_end * stride] = make_float4(emit.x, emit.y, emit.z, 0.f);
-        s_rem[slot] = (uint16_t)((D - 1 - k_end) | (res == kLight ? kEndLight : 0) |
-                                 (ps.nonfinite ? kEndNonfinite : 0));
+        // dead depths left: D-1-k_end, plus depth k_end's own draws when the
+        // path died there (bounce<.., true> left them to the fast-forward)
+        const int rem = D - 1 - k_end + (res != kAlive ? 1 : 0);
+        s_rem[slot] = (uint16_t)(rem | (res == kLight ? kEndLight : 0) | (ps.nonfinite ? kEndNonfinite : 0));
 #else
         const f3 c = path_radiance(res, k_end, emit, ps.nonfinite, hist, stride);
         s_r[slot] = s_r[slot] + c.x;  // cols += sumtotl (MapperPathTracer.cxx:350), in sample order
         s_g[slot] = s_g[slot] + c.y;
         s_b[slot] = s_b[slot] + c.z;
-        s_rem[slot] = (uint16_t)(D - 1 - k_end);
+        s_rem[slot] = (uint16_t)(D - 1 - k_end + (res != kAlive ? 1 : 0));
 #endif
         s_samples[slot] = s_samples[slot] + 1u;
         s_live[slot] = s_live[slot] + (uint32_t)(k_end + 1);
