@@ -286,6 +286,43 @@ RTP_DEV float dot_m(const float* x, const float* y) {  // vtkm::Dot without the 
   else return 0.0f;
 }
 
+// Packed pairs (v_pk_mul_f32 / v_pk_add_f32 round each half like the scalar
+// instruction), used to run a parallelogram's two triangles side by side.
+typedef float f2v __attribute__((ext_vector_type(2)));
+template <int ME, int I>
+RTP_DEV f2v cross_c2(const f2v (&a)[3], const float* e) {  // component I of cross(a, e), e shared
+  constexpr int i1 = (I + 1) % 3, i2 = (I + 2) % 3;
+  constexpr bool p = (ME >> i2) & 1, q = (ME >> i1) & 1;
+  if constexpr (p && q) return a[i1] * e[i2] - a[i2] * e[i1];
+  else if constexpr (p) return a[i1] * e[i2];
+  else if constexpr (q) return -(a[i2] * e[i1]);
+  else return f2v{0.0f, 0.0f};
+}
+template <int M>
+RTP_DEV f2v dot_m2(const f2v (&x)[3], const float* y) {  // dot_m with a shared right-hand side
+  constexpr bool b0 = M & 1, b1 = (M >> 1) & 1, b2 = (M >> 2) & 1;
+  if constexpr (b0 && b1 && b2) return (x[0] * y[0] + x[1] * y[1]) + x[2] * y[2];
+  else if constexpr (b0 && b1) return x[0] * y[0] + x[1] * y[1];
+  else if constexpr (b0 && b2) return x[0] * y[0] + x[2] * y[2];
+  else if constexpr (b1 && b2) return x[1] * y[1] + x[2] * y[2];
+  else if constexpr (b0) return x[0] * y[0];
+  else if constexpr (b1) return x[1] * y[1];
+  else if constexpr (b2) return x[2] * y[2];
+  else return f2v{0.0f, 0.0f};
+}
+template <int M>
+RTP_DEV f2v dot_m2l(const float* x, const f2v (&y)[3]) {  // dot_m with a shared left-hand side
+  constexpr bool b0 = M & 1, b1 = (M >> 1) & 1, b2 = (M >> 2) & 1;
+  if constexpr (b0 && b1 && b2) return (x[0] * y[0] + x[1] * y[1]) + x[2] * y[2];
+  else if constexpr (b0 && b1) return x[0] * y[0] + x[1] * y[1];
+  else if constexpr (b0 && b2) return x[0] * y[0] + x[2] * y[2];
+  else if constexpr (b1 && b2) return x[1] * y[1] + x[2] * y[2];
+  else if constexpr (b0) return x[0] * y[0];
+  else if constexpr (b1) return x[1] * y[1];
+  else if constexpr (b2) return x[2] * y[2];
+  else return f2v{0.0f, 0.0f};
+}
+
 template <int K>
 RTP_DEV bool quad_hit_masked(const DevQuad& Q, f3 o, f3 d, float& t_out) {
   constexpr int M01 = kQuadKind[K].m01, M03 = kQuadKind[K].m03, M21 = kQuadKind[K].m21, M23 = kQuadKind[K].m23;
@@ -294,30 +331,40 @@ RTP_DEV bool quad_hit_masked(const DevQuad& Q, f3 o, f3 d, float& t_out) {
   const float P[3] = {cross_c<M03, 0>(dv, Q.e03), cross_c<M03, 1>(dv, Q.e03), cross_c<M03, 2>(dv, Q.e03)};
   const float det = dot_m<M01 & MP>(Q.e01, P);
   const float inv_det = rcp_det(det);
-  const float T[3] = {o.x - Q.v00[0], o.y - Q.v00[1], o.z - Q.v00[2]};
+  if (Q.para) {
+    // exact parallelogram (e21 == -e03, e23 == -e01 bit for bit): Pp == -P,
+    // detp == det, Qp == -cross(Tp, e01), so the second triangle is the first
+    // one's arithmetic on Tp = o - v11 with both results negated (negation
+    // commutes with rounding).  Half .x is the (v00) triangle, .y the (v11)
+    // one; both always evaluated, branch-free.
+    static_assert(M21 == M03 && M23 == M01, "kinds pair e21 with e03 and e23 with e01");
+    const float ov[3] = {o.x, o.y, o.z};
+    const f2v T2[3] = {f2v{ov[0], ov[0]} - f2v{Q.vv[0][0], Q.vv[0][1]},
+                       f2v{ov[1], ov[1]} - f2v{Q.vv[1][0], Q.vv[1][1]},
+                       f2v{ov[2], ov[2]} - f2v{Q.vv[2][0], Q.vv[2][1]}};
+    const f2v al2 = dot_m2<MP>(T2, P) * inv_det;  // (alpha, -ap)
+    const f2v Q2[3] = {cross_c2<M01, 0>(T2, Q.e01), cross_c2<M01, 1>(T2, Q.e01), cross_c2<M01, 2>(T2, Q.e01)};
+    const f2v be2 = dot_m2l<MQ>(dv, Q2) * inv_det;  // (beta, -bp)
+    const float Qv[3] = {Q2[0].x, Q2[1].x, Q2[2].x};
+    const float t = dot_m<M03 & MQ>(Q.e03, Qv) * inv_det;
+    const float alpha = al2.x, beta = be2.x, ap = -al2.y, bp = -be2.y;
+    bool ok = !(fabsf(det) < kEps) && !(alpha < 0.0f) && !(beta < 0.0f) && !(t < 0.0f);
+    const bool second = (alpha + beta) > 1.0f;
+    ok = ok && (!second || (!(ap < 0.0f) && !(bp < 0.0f)));
+    t_out = t;
+    return ok;
+  }
+  const float T[3] = {o.x - Q.vv[0][0], o.y - Q.vv[1][0], o.z - Q.vv[2][0]};
   const float alpha = dot_m<MP>(T, P) * inv_det;
   const float Qv[3] = {cross_c<M01, 0>(T, Q.e01), cross_c<M01, 1>(T, Q.e01), cross_c<M01, 2>(T, Q.e01)};
   const float beta = dot_m<MQ>(dv, Qv) * inv_det;
   const float t = dot_m<M03 & MQ>(Q.e03, Qv) * inv_det;
   bool ok = !(fabsf(det) < kEps) && !(alpha < 0.0f) && !(beta < 0.0f) && !(t < 0.0f);
   if (ok && (alpha + beta) > 1.0f) {
-    if (Q.para) {
-      // exact parallelogram: e21 == -e03 and e23 == -e01 bit for bit, so
-      // Pp == -P, detp == det (the same products with both factors negated),
-      // Qp == -cross(Tp, e01); negation commutes with rounding.
-      static_assert(M21 == M03 && M23 == M01, "kinds pair e21 with e03 and e23 with e01");
-      const float Tp[3] = {o.x - Q.v11[0], o.y - Q.v11[1], o.z - Q.v11[2]};
-      const float ap = -dot_m<MP>(Tp, P) * inv_det;
-      const float Qp[3] = {cross_c<M01, 0>(Tp, Q.e01), cross_c<M01, 1>(Tp, Q.e01), cross_c<M01, 2>(Tp, Q.e01)};
-      const float bp = -dot_m<MQ>(dv, Qp) * inv_det;
-      ok = !(ap < 0.0f) && !(bp < 0.0f);
-      t_out = t;
-      return ok;
-    }
     const float Pp[3] = {cross_c<M21, 0>(dv, Q.e21), cross_c<M21, 1>(dv, Q.e21), cross_c<M21, 2>(dv, Q.e21)};
     const float detp = dot_m<M23 & MPp>(Q.e23, Pp);
     const float inv_detp = rcp_det(detp);
-    const float Tp[3] = {o.x - Q.v11[0], o.y - Q.v11[1], o.z - Q.v11[2]};
+    const float Tp[3] = {o.x - Q.vv[0][1], o.y - Q.vv[1][1], o.z - Q.vv[2][1]};
     const float ap = dot_m<MPp>(Tp, Pp) * inv_detp;
     const float Qp[3] = {cross_c<M23, 0>(Tp, Q.e23), cross_c<M23, 1>(Tp, Q.e23), cross_c<M23, 2>(Tp, Q.e23)};
     const float bp = dot_m<MQp>(dv, Qp) * inv_detp;

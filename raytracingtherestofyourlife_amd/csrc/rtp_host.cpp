@@ -81,10 +81,9 @@ uint32_t which_threshold(int w) {
 
 void fill_quad(rtp::DevQuad& Q, v3 q, v3 r, v3 s, v3 t) {
   std::memset(&Q, 0, sizeof(Q));
-  st(Q.v00, q);
+  for (int k = 0; k < 3; k++) Q.vv[k][0] = (&q.x)[k], Q.vv[k][1] = (&s.x)[k];
   st(Q.e01, sub(r, q));
   st(Q.e03, sub(t, q));
-  st(Q.v11, s);
   st(Q.e21, sub(r, s));
   st(Q.e23, sub(t, s));
   st(Q.n, normalize(cross(sub(r, q), sub(s, q))));  // TriangleNormal(q,r,s), Surface.h:182-183

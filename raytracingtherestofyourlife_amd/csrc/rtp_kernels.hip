@@ -151,6 +151,26 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d) {
   Hit h{3.40282347e+38f, -1, 0};
   int best = 0x7fffffff;
   const float tmin = 0.001f;
+#if RTP_DUP >= 11 && RTP_DUP <= 14
+  {  // cost attribution of the closest-hit parts (see RTP_DUP)
+    Hit h2 = h;
+    int b2 = best;
+    f3 o2 = o;
+    RTP_OPQ(o2.x);
+    if (RTP_DUP == 11) {
+      scan_kind<1>(sc, 0, o2, d, h2, b2); scan_kind<2>(sc, 1, o2, d, h2, b2); scan_kind<3>(sc, 2, o2, d, h2, b2);
+      scan_kind<4>(sc, 3, o2, d, h2, b2); scan_kind<5>(sc, 4, o2, d, h2, b2); scan_kind<6>(sc, 5, o2, d, h2, b2);
+    } else if (RTP_DUP == 12) {
+      scan_kind<7>(sc, 6, o2, d, h2, b2); scan_kind<8>(sc, 7, o2, d, h2, b2); scan_kind<9>(sc, 8, o2, d, h2, b2);
+    } else if (RTP_DUP == 13) {
+      scan_kind<0>(sc, 9, o2, d, h2, b2);
+    } else {
+      float t;
+      if (sphere_hit(o2, d, tmin, h2.t, ld3(sc->spheres[0].c), sc->spheres[0].rr, t)) h2.t = t;
+    }
+    if (__float_as_uint(h2.t) == 0x7fc12345u) h.idx ^= 1;
+  }
+#endif
   // scan order of the host's grouping: kinds 1..kQuadKinds-1, then 0
   scan_kind<1>(sc, 0, o, d, h, best);
   scan_kind<2>(sc, 1, o, d, h, best);

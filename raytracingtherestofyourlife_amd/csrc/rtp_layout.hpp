@@ -34,8 +34,9 @@ constexpr QuadKindMasks kQuadKind[kQuadKinds] = {
 // One quad of the Lagae-Dutre test (Surface.h:31-161) with v00=q, v10=r,
 // v11=s, v01=t.  Read with uniform (scalar) loads.
 struct alignas(16) DevQuad {
-  float v00[3], e01[3], e03[3];  // e01 = v10-v00, e03 = v01-v00
-  float v11[3], e21[3], e23[3];  // e21 = v10-v11, e23 = v01-v11
+  float vv[3][2];                // (v00[k], v11[k]) interleaved: one SGPR pair per axis for packed math
+  float e01[3], e03[3];          // e01 = v10-v00, e03 = v01-v00
+  float e21[3], e23[3];          // e21 = v10-v11, e23 = v01-v11
   float n[3];                    // Normalize(TriangleNormal(q,r,s)), unflipped
   float alb[3];                  // tex[texType[texIdx]]
   int32_t mt;                    // matType[matIdx]
