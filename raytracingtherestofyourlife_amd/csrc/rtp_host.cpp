@@ -255,7 +255,7 @@ rtp_status rtp_create(int32_t device, rtp_context** out) {
   }
   e = hipMalloc(&c->d_progress, 8);
   if (e != hipSuccess) {
-    hipFree(c->d_scene);
+    (void)hipFree(c->d_scene);
     delete c;
     return hip_fail(e, "hipMalloc(progress)");
   }
@@ -267,16 +267,16 @@ rtp_status rtp_create(int32_t device, rtp_context** out) {
 
 void rtp_destroy(rtp_context* c) {
   if (!c) return;
-  hipSetDevice(c->device);
-  if (c->d_scene) hipFree(c->d_scene);
-  if (c->d_hist) hipFree(c->d_hist);
-  if (c->d_dbg) hipFree(c->d_dbg);
-  if (c->d_progress) hipFree(c->d_progress);
-  if (c->d_nodes) hipFree(c->d_nodes);
-  if (c->d_sph_geom) hipFree(c->d_sph_geom);
-  if (c->d_sph_all) hipFree(c->d_sph_all);
-  if (c->ev0) hipEventDestroy(c->ev0);
-  if (c->ev1) hipEventDestroy(c->ev1);
+  (void)hipSetDevice(c->device);
+  if (c->d_scene) (void)hipFree(c->d_scene);
+  if (c->d_hist) (void)hipFree(c->d_hist);
+  if (c->d_dbg) (void)hipFree(c->d_dbg);
+  if (c->d_progress) (void)hipFree(c->d_progress);
+  if (c->d_nodes) (void)hipFree(c->d_nodes);
+  if (c->d_sph_geom) (void)hipFree(c->d_sph_geom);
+  if (c->d_sph_all) (void)hipFree(c->d_sph_all);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
 }
 
@@ -489,6 +489,11 @@ rtp_status check_render_args(rtp_context* c, const rtp_camera* cam, int32_t nx, 
   // depthcount < 1 makes the reference read emitted[(depth-1)*N] out of range
   // (MapperPathTracer.cxx:328-331); rejected here.
   if (depth < 1) return fail(RTP_ERR_INVALID_ARGUMENT, "render: depthcount must be >= 1");
+  // device-side bookkeeping limits: the pool kernel packs the remaining dead
+  // depths into 14 bits and counts a wave's finished samples (<= 256 * spp)
+  // in 32-bit signed cursors
+  if (depth > rtp::kMaxDepth) return fail(RTP_ERR_INVALID_ARGUMENT, "render: depthcount must be <= 16383");
+  if (spp > rtp::kMaxSpp) return fail(RTP_ERR_INVALID_ARGUMENT, "render: samplecount must be <= 8388607");
   return RTP_OK;
 }
 
@@ -532,7 +537,7 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
   {
     const char* e = getenv("RTP_DEBUG_STATS");
     if (e && (e[0] == '1' || e[0] == '2') && variant == 2) {  // 2: timestamps in the production kernel
-      if (c->d_dbg) hipFree(c->d_dbg);
+      if (c->d_dbg) (void)hipFree(c->d_dbg);
       c->d_dbg = nullptr;
       HIP_TRY(hipMalloc(&c->d_dbg, (size_t)waves * rtp::kDbgCounters * 8));
       HIP_TRY(hipMemsetAsync(c->d_dbg, 0, (size_t)waves * rtp::kDbgCounters * 8, stream));
@@ -568,10 +573,10 @@ rtp_status render_host(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_
   double ms = 0;
   std::vector<uint32_t> live(npix);
   auto cleanup = [&]() {
-    if (d_ids) hipFree(d_ids);
-    if (d_out) hipFree(d_out);
-    if (d_seed) hipFree(d_seed);
-    if (d_live) hipFree(d_live);
+    if (d_ids) (void)hipFree(d_ids);
+    if (d_out) (void)hipFree(d_out);
+    if (d_seed) (void)hipFree(d_seed);
+    if (d_live) (void)hipFree(d_live);
   };
   hipError_t e = hipMalloc(&d_out, (size_t)npix * 16);
   if (e == hipSuccess) e = hipMalloc(&d_live, (size_t)npix * 4);
@@ -730,8 +735,8 @@ rtp_status rtp_verify_fast_math(rtp_context* c, int32_t kind, uint32_t lo_bits, 
   uint32_t first = 0;
   HIP_TRY(hipMemcpy(&bad, d_bad, 8, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(&first, d_first, 4, hipMemcpyDeviceToHost));
-  hipFree(d_bad);
-  hipFree(d_first);
+  (void)hipFree(d_bad);
+  (void)hipFree(d_first);
   *mismatches = bad;
   if (first_bad) *first_bad = first;
   return RTP_OK;

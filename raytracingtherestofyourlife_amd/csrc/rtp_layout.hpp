@@ -11,6 +11,8 @@
 namespace rtp {
 
 constexpr int kMaxQuads = 256;
+constexpr int kMaxDepth = 16383;    // remaining dead depths fit the 14-bit field of the pool's slots
+constexpr int kMaxSpp = 8388607;    // 256 slots * spp fits the pool's 32-bit sample cursors
 constexpr int kMaxSpheres = 256;          // held inline in DevScene (scalar loads)
 constexpr int kMaxSpheresBvh = 1 << 22;   // spheres behind the BVH (global memory)
 constexpr int kBvhMinSpheres = 9;         // scenes with more spheres use the BVH

@@ -188,6 +188,23 @@ def test_invalid_arguments(device, rtp):
         device.render(bad, 4, 4, 1, 1)
     with pytest.raises(rtp.RtpError):
         device.render_pixels(cam, 4, 4, 1, 1, np.array([16], dtype=np.int64))
+    with pytest.raises(rtp.RtpError):  # device bookkeeping limits (rtp_layout.hpp kMaxDepth / kMaxSpp)
+        device.render(cam, 4, 4, 1, 16384)
+    with pytest.raises(rtp.RtpError):
+        device.render(cam, 4, 4, 8388608, 1)
+
+
+def test_empty_pixel_list_and_zero_spp(device, rtp):
+    import torch
+
+    cam = rtp.default_camera()
+    out = torch.full((4, 4), 7.0, dtype=torch.float32, device="cuda")
+    device.render_device(cam, 8, 8, 4, 5, out.data_ptr(), pixel_begin=0, pixel_count=0,
+                         stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert bool((out == 7.0).all())  # nothing written
+    rgba, _ = device.render(cam, 8, 8, 0, 5)  # spp 0: the canvas is zero
+    assert not rgba[:, :3].any()
 
 
 def test_c3_many_spheres_bvh_subset(oracle, device, rtp):
