@@ -166,22 +166,34 @@ const FfTables& ff_tables(int device) {
 }
 
 // Sphere BVH (replaces the VTK-m LinearBVH of buildBVH, MapperPathTracer.cxx:
-// 437-449, for scenes with many spheres).  Median split on the longest axis
-// of the centroid bounds, ties broken by sphere index (deterministic), leaves
-// of <= kBvhLeafSize spheres, depth-first "threaded" layout.  The boxes only
-// cull: each sphere box is padded by 0.2% of its radius + 1e-5 so that every
-// point the device's float sphere test can return lies inside it, and the
-// kernel compares against a slack-widened [0, t_best] interval.  The closest
-// hit is the lexicographic min of (t, kind, index) whatever the visit order.
+// 437-449, for scenes with many spheres).  Binned SAH (16 bins per axis) with
+// deterministic partitions, leaves of <= kBvhLeafSize spheres.  The tree is
+// flattened eight times, once per ray-direction octant: each copy is a
+// depth-first "threaded" array (hit: next node; miss or leaf done: skip) that
+// visits the child on the near side of the split axis first, so a lane walks
+// near-to-far without a stack and the closest-hit bound culls early.  Boxes
+// only cull: each sphere box is padded by 0.2% of its radius + 1e-5 so that
+// every point the device's float sphere test can return lies inside it, and
+// the kernel compares against a slack-widened [0, t_best] interval.  The
+// closest hit is the lexicographic min of (t, kind, index) whatever the order.
 struct BvhPrim {
   float lo[3], hi[3], cen[3];
   int32_t idx;
 };
+struct TNode {
+  float lo[3], hi[3];
+  int axis = 0, left = -1, right = -1, first = 0, count = 0;
+};
 
-int32_t bvh_build(std::vector<BvhPrim>& P, int b, int e, std::vector<rtp::BvhNode>& out, std::vector<int32_t>& order) {
-  const int32_t me = (int32_t)out.size();
-  out.push_back(rtp::BvhNode{});
-  rtp::BvhNode nd{};
+float half_area(const float lo[3], const float hi[3]) {
+  const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+  return dx * dy + dy * dz + dz * dx;
+}
+
+int bvh_build(std::vector<BvhPrim>& P, int b, int e, std::vector<TNode>& T, std::vector<int32_t>& order) {
+  const int me = (int)T.size();
+  T.emplace_back();
+  TNode nd;
   float clo[3], chi[3];
   for (int k = 0; k < 3; k++) {
     nd.lo[k] = clo[k] = INFINITY;
@@ -194,24 +206,86 @@ int32_t bvh_build(std::vector<BvhPrim>& P, int b, int e, std::vector<rtp::BvhNod
       clo[k] = std::min(clo[k], P[i].cen[k]);
       chi[k] = std::max(chi[k], P[i].cen[k]);
     }
-  if (e - b <= rtp::kBvhLeafSize) {
-    nd.leaf = ((int32_t)order.size() << 3) | (e - b);
+  const int n = e - b;
+  if (n <= rtp::kBvhLeafSize) {
+    nd.first = (int)order.size();
+    nd.count = n;
     for (int i = b; i < e; i++) order.push_back(P[i].idx);
+    T[me] = nd;
+    return me;
+  }
+  // binned SAH
+  constexpr int kBins = 16;
+  int best_ax = -1, best_split = 0;
+  float best_cost = INFINITY;
+  for (int ax = 0; ax < 3; ax++) {
+    const float ext = chi[ax] - clo[ax];
+    if (!(ext > 0)) continue;
+    int cnt[kBins] = {};
+    float blo[kBins][3], bhi[kBins][3];
+    for (int j = 0; j < kBins; j++)
+      for (int k = 0; k < 3; k++) blo[j][k] = INFINITY, bhi[j][k] = -INFINITY;
+    for (int i = b; i < e; i++) {
+      int j = (int)((P[i].cen[ax] - clo[ax]) / ext * kBins);
+      j = std::min(kBins - 1, std::max(0, j));
+      cnt[j]++;
+      for (int k = 0; k < 3; k++) blo[j][k] = std::min(blo[j][k], P[i].lo[k]), bhi[j][k] = std::max(bhi[j][k], P[i].hi[k]);
+    }
+    for (int s = 1; s < kBins; s++) {  // split between bins s-1 and s
+      float llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+      float rlo[3] = {INFINITY, INFINITY, INFINITY}, rhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+      int nl = 0, nr = 0;
+      for (int j = 0; j < kBins; j++) {
+        if (!cnt[j]) continue;
+        float* lo = j < s ? llo : rlo;
+        float* hi = j < s ? lhi : rhi;
+        (j < s ? nl : nr) += cnt[j];
+        for (int k = 0; k < 3; k++) lo[k] = std::min(lo[k], blo[j][k]), hi[k] = std::max(hi[k], bhi[j][k]);
+      }
+      if (!nl || !nr) continue;
+      const float cost = nl * half_area(llo, lhi) + nr * half_area(rlo, rhi);
+      if (cost < best_cost) best_cost = cost, best_ax = ax, best_split = s;
+    }
+  }
+  int mid;
+  if (best_ax >= 0) {
+    const int ax = best_ax;
+    const float ext = chi[ax] - clo[ax];
+    auto bin = [&](const BvhPrim& x) {
+      return std::min(kBins - 1, std::max(0, (int)((x.cen[ax] - clo[ax]) / ext * kBins)));
+    };
+    mid = (int)(std::stable_partition(P.begin() + b, P.begin() + e, [&](const BvhPrim& x) { return bin(x) < best_split; }) -
+                P.begin());
+    nd.axis = ax;
+  } else {  // coincident centroids: median split by index
+    std::sort(P.begin() + b, P.begin() + e, [](const BvhPrim& x, const BvhPrim& y) { return x.idx < y.idx; });
+    mid = b + n / 2;
+    nd.axis = 0;
+  }
+  nd.left = bvh_build(P, b, mid, T, order);
+  nd.right = bvh_build(P, mid, e, T, order);
+  T[me] = nd;
+  return me;
+}
+
+// threaded flattening for one octant (bit k set: direction component k < 0)
+void bvh_flatten(const std::vector<TNode>& T, int t, int oct, std::vector<rtp::BvhNode>& out) {
+  const int me = (int)out.size();
+  out.emplace_back();
+  rtp::BvhNode nd{};
+  const TNode& s = T[t];
+  std::memcpy(nd.lo, s.lo, sizeof(nd.lo));
+  std::memcpy(nd.hi, s.hi, sizeof(nd.hi));
+  if (s.left < 0) {
+    nd.leaf = (s.first << 3) | s.count;
   } else {
-    int ax = 0;
-    for (int k = 1; k < 3; k++)
-      if (chi[k] - clo[k] > chi[ax] - clo[ax]) ax = k;
-    std::sort(P.begin() + b, P.begin() + e, [ax](const BvhPrim& x, const BvhPrim& y) {
-      return x.cen[ax] < y.cen[ax] || (x.cen[ax] == y.cen[ax] && x.idx < y.idx);
-    });
-    const int mid = b + (e - b) / 2;
-    bvh_build(P, b, mid, out, order);
-    bvh_build(P, mid, e, out, order);
+    const bool neg = (oct >> s.axis) & 1;  // moving toward lower coordinates: right (upper) child first
+    bvh_flatten(T, neg ? s.right : s.left, oct, out);
+    bvh_flatten(T, neg ? s.left : s.right, oct, out);
     nd.leaf = 0;
   }
   nd.skip = (int32_t)out.size();
   out[me] = nd;
-  return me;
 }
 
 }  // namespace
@@ -384,7 +458,13 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
       P[k].idx = k;
     }
     std::vector<int32_t> order;
-    bvh_build(P, 0, s->n_spheres, nodes, order);
+    std::vector<TNode> tree;
+    bvh_build(P, 0, s->n_spheres, tree, order);
+    for (int oct = 0; oct < 8; oct++) {  // 8 copies of n_nodes entries, indices local to each copy
+      std::vector<rtp::BvhNode> one;
+      bvh_flatten(tree, 0, oct, one);
+      nodes.insert(nodes.end(), one.begin(), one.end());
+    }
     geom.resize(order.size());
     for (size_t j = 0; j < order.size(); j++) {
       const rtp::DevSphere& S = sph[order[j]];
@@ -393,7 +473,7 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
       geom[j].rr = S.rr;
       geom[j].orig = order[j];
     }
-    h->n_nodes = (int32_t)nodes.size();
+    h->n_nodes = (int32_t)tree.size();
   }
   h->n_spheres = s->n_spheres;
   // lights (MapperPathTracer.cxx:141-148): light quad = light_box_pointids[1..4]

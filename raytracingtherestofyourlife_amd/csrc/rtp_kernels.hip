@@ -113,9 +113,11 @@ RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
   const float ix = __builtin_amdgcn_rcpf(fabsf(d.x) < 1e-20f ? copysignf(1e-20f, d.x) : d.x);
   const float iy = __builtin_amdgcn_rcpf(fabsf(d.y) < 1e-20f ? copysignf(1e-20f, d.y) : d.y);
   const float iz = __builtin_amdgcn_rcpf(fabsf(d.z) < 1e-20f ? copysignf(1e-20f, d.z) : d.z);
-  const BvhNode* __restrict__ nodes = sc->nodes;
-  const DevSphereG* __restrict__ geom = sc->sph_geom;
   const int nn = sc->n_nodes;
+  // the copy of the tree ordered near-to-far for this ray's direction octant
+  const int oct = (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0);
+  const BvhNode* __restrict__ nodes = sc->nodes + (int64_t)oct * nn;
+  const DevSphereG* __restrict__ geom = sc->sph_geom;
   int ni = 0;
   while (ni < nn) {
     const float4 a = *reinterpret_cast<const float4*>(&nodes[ni].lo[0]);

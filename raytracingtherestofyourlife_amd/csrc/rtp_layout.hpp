@@ -16,7 +16,10 @@ constexpr int kMaxSpp = 8388607;    // 256 slots * spp fits the pool's 32-bit sa
 constexpr int kMaxSpheres = 256;          // held inline in DevScene (scalar loads)
 constexpr int kMaxSpheresBvh = 1 << 22;   // spheres behind the BVH (global memory)
 constexpr int kBvhMinSpheres = 9;         // scenes with more spheres use the BVH
-constexpr int kBvhLeafSize = 4;
+#ifndef RTP_BVH_LEAF
+#define RTP_BVH_LEAF 1  // measured best on C3: 1 < 2 < 4 < 7 (367 / 407 / 469 / 564 ms at 16 spp)
+#endif
+constexpr int kBvhLeafSize = RTP_BVH_LEAF;  // leaf size bound (<= 7: 3-bit count field)
 
 // Zero-structure kinds of quads: the masks of the nonzero components of the
 // edge vectors (e01, e03, e21, e23).  A kind's test (quad_hit_masked) drops
@@ -96,9 +99,9 @@ struct alignas(16) DevScene {
   uint32_t which_t1;  // smallest hash with which >= 2   (PdfWorklet.h:20)
   uint32_t which_t2;  // smallest hash with which == 3
   float ior;
-  int32_t n_nodes;                 // BVH scenes (n_spheres >= kBvhMinSpheres)
+  int32_t n_nodes;                 // BVH scenes (n_spheres >= kBvhMinSpheres): nodes per octant copy
   int32_t pad[3];
-  const BvhNode* nodes;
+  const BvhNode* nodes;            // 8 * n_nodes: one threaded copy per ray-direction octant
   const DevSphereG* sph_geom;      // BVH leaf order
   const DevSphere* sph_all;        // scene order (materials of the hit sphere)
   DevLights light;
