@@ -331,13 +331,14 @@ RTP_DEV bool quad_hit_masked(const DevQuad& Q, f3 o, f3 d, float& t_out) {
   const float P[3] = {cross_c<M03, 0>(dv, Q.e03), cross_c<M03, 1>(dv, Q.e03), cross_c<M03, 2>(dv, Q.e03)};
   const float det = dot_m<M01 & MP>(Q.e01, P);
   const float inv_det = rcp_det(det);
-  if (Q.para) {
+  // (a parallelogram has e21 == -e03 and e23 == -e01, so only kinds whose
+  // masks pair up can hold one)
+  if constexpr (M21 == M03 && M23 == M01) if (Q.para) {
     // exact parallelogram (e21 == -e03, e23 == -e01 bit for bit): Pp == -P,
     // detp == det, Qp == -cross(Tp, e01), so the second triangle is the first
     // one's arithmetic on Tp = o - v11 with both results negated (negation
     // commutes with rounding).  Half .x is the (v00) triangle, .y the (v11)
     // one; both always evaluated, branch-free.
-    static_assert(M21 == M03 && M23 == M01, "kinds pair e21 with e03 and e23 with e01");
     const float ov[3] = {o.x, o.y, o.z};
     const f2v T2[3] = {f2v{ov[0], ov[0]} - f2v{Q.vv[0][0], Q.vv[0][1]},
                        f2v{ov[1], ov[1]} - f2v{Q.vv[1][0], Q.vv[1][1]},
@@ -386,6 +387,7 @@ RTP_DEV bool quad_hit(const DevQuad& Q, f3 o, f3 d, float& t_out) {
     case 7: return quad_hit_masked<7>(Q, o, d, t_out);
     case 8: return quad_hit_masked<8>(Q, o, d, t_out);
     case 9: return quad_hit_masked<9>(Q, o, d, t_out);
+    case 10: return quad_hit_masked<10>(Q, o, d, t_out);
     default: return quad_hit_masked<0>(Q, o, d, t_out);
   }
 }

@@ -165,7 +165,7 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d) {
     } else if (RTP_DUP == 12) {
       scan_kind<7>(sc, 6, o2, d, h2, b2); scan_kind<8>(sc, 7, o2, d, h2, b2); scan_kind<9>(sc, 8, o2, d, h2, b2);
     } else if (RTP_DUP == 13) {
-      scan_kind<0>(sc, 9, o2, d, h2, b2);
+      scan_kind<0>(sc, 10, o2, d, h2, b2);
     } else {
       float t;
       if (sphere_hit(o2, d, tmin, h2.t, ld3(sc->spheres[0].c), sc->spheres[0].rr, t)) h2.t = t;
@@ -183,8 +183,9 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d) {
   scan_kind<7>(sc, 6, o, d, h, best);
   scan_kind<8>(sc, 7, o, d, h, best);
   scan_kind<9>(sc, 8, o, d, h, best);
-  scan_kind<0>(sc, 9, o, d, h, best);
-  static_assert(kQuadKinds == 10, "closest_hit scans every kind");
+  scan_kind<10>(sc, 9, o, d, h, best);
+  scan_kind<0>(sc, 10, o, d, h, best);
+  static_assert(kQuadKinds == 11, "closest_hit scans every kind");
   if constexpr (kBvh) {
     spheres_bvh(sc, o, d, h);
   } else {

@@ -26,15 +26,17 @@ constexpr int kBvhLeafSize = RTP_BVH_LEAF;  // leaf size bound (<= 7: 3-bit coun
 // every product with a structurally zero component at compile time; the host
 // assigns the kind from exact zeros.  Kind 0 is the general quad; 1..6 are
 // axis-aligned rectangles (e01 along I, e03 along J); 7..9 are the faces of
-// boxes rotated about y (edges in the xz-plane or along y).
-constexpr int kQuadKinds = 10;
+// boxes rotated about y (edges in the xz-plane or along y); 10 is a quad with
+// general first-triangle edges and a flat second triangle.
+constexpr int kQuadKinds = 11;
 struct QuadKindMasks {
   int m01, m03, m21, m23;
 };
 constexpr QuadKindMasks kQuadKind[kQuadKinds] = {
     {7, 7, 7, 7},                                                               // 0 general
     {1, 2, 2, 1}, {1, 4, 4, 1}, {2, 1, 1, 2}, {2, 4, 4, 2}, {4, 1, 1, 4}, {4, 2, 2, 4},  // 1..6 axis-aligned
-    {5, 2, 2, 5}, {2, 5, 5, 2}, {5, 5, 5, 5}};                                  // 7..9 rotated about y
+    {5, 2, 2, 5}, {2, 5, 5, 2}, {5, 5, 5, 5},                                  // 7..9 rotated about y
+    {7, 7, 5, 5}};  // 10: the small box's top (CornellBox.cpp's y=333 vertex): only e21/e23 are flat
 
 // One quad of the Lagae-Dutre test (Surface.h:31-161) with v00=q, v10=r,
 // v11=s, v01=t.  Read with uniform (scalar) loads.
