@@ -45,6 +45,9 @@
 #ifndef RTP_FAIR_READY
 #define RTP_FAIR_READY 1  // pool kernel: lagging pixels jump the READY queue
 #endif
+#ifndef RTP_QSHADE_LDS
+#define RTP_QSHADE_LDS 1  // pool kernel: quads' shading data gathered from LDS
+#endif
 #ifndef RTP_DEFER_RADIANCE
 #define RTP_DEFER_RADIANCE 1  // pool kernel: radiance product in the fast-forward batch
 #endif
@@ -233,9 +236,13 @@ RTP_DEV unsigned long long stamp(bool on) { return on ? __builtin_amdgcn_s_memti
 // kDeferDead: a path that misses or hits the light at depth k leaves its
 // depth-k draws (which + generator, exactly one dead step) to the caller's
 // fast-forward instead of drawing them here.
+// qshade (nullable): the block's LDS copy of the quads' shading data
+// (n, alb, mt; kQShadeFloats per quad) so the hit's material is an LDS
+// gather instead of a global one.
+constexpr int kLdsQuads = 64, kQShadeFloats = 8;
 template <bool kBvh, bool kDeferDead = false>
 RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3& emit, float4* __restrict__ hist_d,
-                   int D, unsigned long long* dbg = nullptr) {
+                   int D, unsigned long long* dbg = nullptr, const float* qshade = nullptr) {
   const bool st = dbg != nullptr;
   const unsigned long long t0 = stamp(st);
   const uint32_t t1 = sc->which_t1, t2 = sc->which_t2;
@@ -265,11 +272,18 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
   int mt;
   f3 alb;
   if (h.kind == 0) {
-    const DevQuad& Q = sc->quads[h.idx];
-    hn = ld3(Q.n);
+    if (qshade != nullptr) {
+      const float* r = qshade + h.idx * kQShadeFloats;
+      hn = mk(r[0], r[1], r[2]);
+      alb = mk(r[3], r[4], r[5]);
+      mt = __float_as_int(r[6]);
+    } else {
+      const DevQuad& Q = sc->quads[h.idx];
+      hn = ld3(Q.n);
+      mt = Q.mt;
+      alb = ld3(Q.alb);
+    }
     if (dot(hn, dir) > 0.f) hn = neg(hn);  // Surface.h:184-185
-    mt = Q.mt;
-    alb = ld3(Q.alb);
   } else {
     const DevSphere& S = kBvh ? sc->sph_all[h.idx] : sc->spheres[h.idx];
     hn = mk((hp.x - S.c[0]) / S.r, (hp.y - S.c[1]) / S.r, (hp.z - S.c[2]) / S.r);
@@ -530,10 +544,21 @@ RTP_DEV void set_priority(float lag) {  // s_setprio needs an immediate
 template <bool kStats, bool kBvh>
 __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_pool(const DevScene* __restrict__ sc, KParams p, int n_waves) {
   __shared__ __align__(16) unsigned char smem[kPoolLdsBytes];
+  __shared__ float s_qshade[kLdsQuads * kQShadeFloats];
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
   const int w = blockIdx.x * kWavesPerBlock + wib;  // global wave id
-  if (w >= n_waves) return;                          // whole wave leaves; no block-level barriers are used
+  // the quads' shading data into LDS (the block's only barrier, before any wave leaves)
+  const bool qshade_lds = RTP_QSHADE_LDS && sc->n_quads <= kLdsQuads;
+  if (qshade_lds) {
+    for (int i = threadIdx.x; i < sc->n_quads * kQShadeFloats; i += blockDim.x) {
+      const DevQuad& Q = sc->quads[i / kQShadeFloats];
+      const int f = i % kQShadeFloats;
+      s_qshade[i] = f < 3 ? Q.n[f] : f < 6 ? Q.alb[f - 3] : f == 6 ? __int_as_float(Q.mt) : 0.f;
+    }
+  }
+  __syncthreads();
+  if (w >= n_waves) return;  // whole wave leaves; no block-level barriers follow
   unsigned char* base = smem + (size_t)wib * kPool * kSlotBytes;
   uint32_t* s_seed = reinterpret_cast<uint32_t*>(base);
   float* s_r = reinterpret_cast<float*>(s_seed + kPool);
@@ -746,7 +771,8 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_poo
     unsigned long long tbnc = ta;
     if (has_path) {
       f3 emit = mk(0.f, 0.f, 0.f);
-      const int res = bounce<kBvh, true>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D, want_dbg ? dbg : nullptr);
+      const int res = bounce<kBvh, true>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D, want_dbg ? dbg : nullptr,
+                                         qshade_lds ? s_qshade : nullptr);
       tbnc = stamp(want_dbg);
       if (res == kAlive && ps.d < D - 1) {
         ps.d++;
