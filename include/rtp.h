@@ -30,6 +30,13 @@
  *
  * Errors: every entry point returns an rtp_status; rtp_last_error() gives a
  * thread-local message (the reference throws vtkm::cont::ErrorBadValue).
+ *
+ * Concurrency: a context is driven by one host thread at a time (like the
+ * reference's mapper).  Its renders are ordered even when they are enqueued
+ * on different streams: each launch waits for the context's previous one,
+ * because they share the context's scratch (path history, progress counter).
+ * rtp_set_scene and rtp_destroy wait for queued renders before replacing or
+ * freeing device buffers.  Use one context per stream for concurrent renders.
  */
 #ifndef RTP_H
 #define RTP_H

@@ -305,7 +305,23 @@ struct rtp_context {
   rtp::DevSphere* d_sph_all = nullptr;
   bool use_bvh = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // Completion of the last launch.  The history buffer and the progress
+  // counter are per-context scratch, so a launch on any stream first waits
+  // for the previous one, and the host waits before it frees or rewrites a
+  // buffer a queued kernel may still read.
+  hipEvent_t done = nullptr;
+  bool pending = false;
 };
+
+namespace {
+rtp_status drain(rtp_context* c) {
+  if (c->pending) {
+    HIP_TRY(hipEventSynchronize(c->done));
+    c->pending = false;
+  }
+  return RTP_OK;
+}
+}  // namespace
 
 extern "C" {
 
@@ -335,6 +351,7 @@ rtp_status rtp_create(int32_t device, rtp_context** out) {
   }
   HIP_TRY(hipEventCreate(&c->ev0));
   HIP_TRY(hipEventCreate(&c->ev1));
+  HIP_TRY(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
   *out = c;
   return RTP_OK;
 }
@@ -342,6 +359,7 @@ rtp_status rtp_create(int32_t device, rtp_context** out) {
 void rtp_destroy(rtp_context* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  (void)drain(c);
   if (c->d_scene) (void)hipFree(c->d_scene);
   if (c->d_hist) (void)hipFree(c->d_hist);
   if (c->d_dbg) (void)hipFree(c->d_dbg);
@@ -351,6 +369,7 @@ void rtp_destroy(rtp_context* c) {
   if (c->d_sph_all) (void)hipFree(c->d_sph_all);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->done) (void)hipEventDestroy(c->done);
   delete c;
 }
 
@@ -509,6 +528,10 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
   h->which_t1 = which_threshold(2);
   h->which_t2 = which_threshold(3);
   hipError_t e = hipSetDevice(c->device);
+  if (c->pending) {  // a queued render may still read the old scene
+    if (e == hipSuccess) e = hipEventSynchronize(c->done);
+    c->pending = false;
+  }
   for (void** p : {(void**)&c->d_nodes, (void**)&c->d_sph_geom, (void**)&c->d_sph_all})
     if (*p && e == hipSuccess) {
       e = hipFree(*p);
@@ -579,6 +602,8 @@ rtp_status check_render_args(rtp_context* c, const rtp_camera* cam, int32_t nx, 
 
 rtp_status ensure_hist(rtp_context* c, size_t bytes) {
   if (bytes <= c->hist_bytes) return RTP_OK;
+  rtp_status rs = drain(c);
+  if (rs != RTP_OK) return rs;
   if (c->d_hist) HIP_TRY(hipFree(c->d_hist));
   c->d_hist = nullptr;
   c->hist_bytes = 0;
@@ -613,6 +638,7 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
     const FfTables& ft = ff_tables(c->device);
     for (int j = 0; j < rtp::kFfTables; j++) p.ff[j] = ft.t[j];
   }
+  if (c->pending) HIP_TRY(hipStreamWaitEvent(stream, c->done, 0));
   HIP_TRY(hipMemsetAsync(c->d_progress, 0, 8, stream));
   {
     const char* e = getenv("RTP_DEBUG_STATS");
@@ -627,6 +653,8 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
   }
   if (kernel_ms) HIP_TRY(hipEventRecord(c->ev0, stream));
   HIP_TRY(rtp_launch_render(c->d_scene, &p, variant, waves, c->use_bvh ? 1 : 0, stream));
+  HIP_TRY(hipEventRecord(c->done, stream));
+  c->pending = true;
   if (kernel_ms) {
     HIP_TRY(hipEventRecord(c->ev1, stream));
     HIP_TRY(hipEventSynchronize(c->ev1));

@@ -158,6 +158,33 @@ def test_render_device_matches_host_path(device, rtp):
     assert np.array_equal(part.cpu().numpy().view(np.uint32), host[1000:1100].view(np.uint32))
 
 
+def test_renders_on_two_streams_share_one_context(device, rtp):
+    """Back-to-back asynchronous renders of one context on two streams (and a
+    scene change while one is queued) are ordered by the context: the
+    per-context history buffer and progress counter are never used by two
+    kernels at once."""
+    import torch
+
+    cam = rtp.default_camera()
+    nx = ny = 96
+    device.set_cornell_box(0)
+    want0 = device.render_pixels(cam, nx, ny, 6, 12, np.arange(nx * ny))[0]
+    device.set_cornell_box(2)
+    want2 = device.render_pixels(cam, nx, ny, 6, 12, np.arange(nx * ny))[0]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    a = torch.zeros((nx * ny, 4), dtype=torch.float32, device="cuda")
+    b = torch.zeros_like(a)
+    c = torch.zeros_like(a)
+    device.set_cornell_box(0)
+    device.render_device(cam, nx, ny, 6, 12, a.data_ptr(), stream=s1.cuda_stream)
+    device.render_device(cam, nx, ny, 6, 12, b.data_ptr(), stream=s2.cuda_stream)
+    device.set_cornell_box(2)  # waits for the queued renders before replacing the scene
+    device.render_device(cam, nx, ny, 6, 12, c.data_ptr(), stream=s1.cuda_stream)
+    torch.cuda.synchronize()
+    for got, want, name in ((a, want0, "stream 1"), (b, want0, "stream 2"), (c, want2, "after set_scene")):
+        assert np.array_equal(got.cpu().numpy().view(np.uint32), want.view(np.uint32)), name
+
+
 def test_mapper_api_runpath(oracle, device, rtp):
     """The reference's own call sequence (main.cc:289-323) through the mirror."""
     cb = rtp.CornellBox()
