@@ -12,6 +12,9 @@
 #include "rtp_layout.hpp"
 
 #define RTP_DEV __device__ __forceinline__
+#ifndef RTP_PARA_BITWISE
+#define RTP_PARA_BITWISE 1
+#endif
 
 namespace rtp {
 
@@ -348,12 +351,24 @@ RTP_DEV bool quad_hit_masked(const DevQuad& Q, f3 o, f3 d, float& t_out) {
     const f2v be2 = dot_m2l<MQ>(dv, Q2) * inv_det;  // (beta, -bp)
     const float Qv[3] = {Q2[0].x, Q2[1].x, Q2[2].x};
     const float t = dot_m<M03 & MQ>(Q.e03, Qv) * inv_det;
-    const float alpha = al2.x, beta = be2.x, ap = -al2.y, bp = -be2.y;
+    const float alpha = al2.x, beta = be2.x;
+#if RTP_PARA_BITWISE
+    // ap < 0 <=> -al2.y < 0 <=> al2.y > 0 (NaN: false both ways; -(+-0) is
+    // not < 0 and +-0 is not > 0), likewise bp; evaluated without short
+    // circuits so no lane mask or max canonicalisation is generated
+    const bool ok1 = !(fabsf(det) < kEps) & !(alpha < 0.0f) & !(beta < 0.0f) & !(t < 0.0f);
+    const bool second = (alpha + beta) > 1.0f;
+    const bool bad2 = (al2.y > 0.0f) | (be2.y > 0.0f);
+    t_out = t;
+    return ok1 & !(second & bad2);
+#else
+    const float ap = -al2.y, bp = -be2.y;
     bool ok = !(fabsf(det) < kEps) && !(alpha < 0.0f) && !(beta < 0.0f) && !(t < 0.0f);
     const bool second = (alpha + beta) > 1.0f;
     ok = ok && (!second || (!(ap < 0.0f) && !(bp < 0.0f)));
     t_out = t;
     return ok;
+#endif
   }
   const float T[3] = {o.x - Q.vv[0][0], o.y - Q.vv[1][0], o.z - Q.vv[2][0]};
   const float alpha = dot_m<MP>(T, P) * inv_det;

@@ -439,7 +439,11 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
       const int kind = (g + 1) % rtp::kQuadKinds;
       h->kind_begin[g] = pos;
       for (const rtp::DevQuad& Q : built)
-        if (Q.kind == kind) h->quads[pos++] = Q;
+        if (Q.kind == kind) {
+          h->quads[pos] = Q;
+          h->quads[pos].key_lo = ((uint32_t)Q.orig << 8) | (uint32_t)pos;  // both < kMaxQuads = 256
+          pos++;
+        }
     }
     h->kind_begin[rtp::kQuadKinds] = pos;
   }

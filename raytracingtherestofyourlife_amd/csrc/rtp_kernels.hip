@@ -69,6 +69,28 @@ struct Hit {
 // returns the lexicographic minimum of (t, index) over the hits, so the quads
 // can be visited grouped by zero-structure kind (one tight loop per kind) as
 // long as equal t is broken by the original index.
+#ifndef RTP_HIT_KEY
+#define RTP_HIT_KEY 1
+#endif
+#if RTP_HIT_KEY
+// The (t, orig) minimum as one unsigned 64-bit key {bits(t), orig << 8 | q}:
+// an accepted t is > 0.001, and positive floats order like their bit
+// patterns, so key order is exactly "t, then reference index".  The scan
+// position q rides in the low bits (orig is unique, so it never decides).
+static_assert(kMaxQuads <= 256, "key_lo packs orig and the scan position in 8 bits each");
+constexpr uint64_t kNoHitKey = (uint64_t)0x7f7fffffu << 32 | 0xffffffffu;  // {FLT_MAX, none}
+template <int K>
+RTP_DEV void scan_kind(const DevScene* __restrict__ sc, int g, f3 o, f3 d, uint64_t& best) {
+  const int b = sc->kind_begin[g], e = sc->kind_begin[g + 1];
+  for (int q = b; q < e; q++) {
+    const DevQuad& Q = sc->quads[q];
+    float t;
+    const bool ok = quad_hit_masked<K>(Q, o, d, t);
+    const uint64_t key = (uint64_t)__float_as_uint(t) << 32 | Q.key_lo;
+    best = (ok && t > 0.001f && key < best) ? key : best;
+  }
+}
+#else
 template <int K>
 RTP_DEV void scan_kind(const DevScene* __restrict__ sc, int g, f3 o, f3 d, Hit& h, int& best) {
   const int b = sc->kind_begin[g], e = sc->kind_begin[g + 1];
@@ -85,6 +107,7 @@ RTP_DEV void scan_kind(const DevScene* __restrict__ sc, int g, f3 o, f3 d, Hit& 
     }
   }
 }
+#endif
 
 // SphereLeafIntersector::hit's accepted root without the tmax test: the
 // reference takes r1 = (-b-sq)/a if tmin < r1 < tmax, else r2 = (-b+sq)/a if
@@ -159,24 +182,50 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d) {
 #if RTP_DUP >= 11 && RTP_DUP <= 14
   {  // cost attribution of the closest-hit parts (see RTP_DUP)
     Hit h2 = h;
+#if RTP_HIT_KEY
+    uint64_t b2 = kNoHitKey;
+#define RTP_SCAN2(K, G) scan_kind<K>(sc, G, o2, d, b2)
+#else
     int b2 = best;
+#define RTP_SCAN2(K, G) scan_kind<K>(sc, G, o2, d, h2, b2)
+#endif
     f3 o2 = o;
     RTP_OPQ(o2.x);
     if (RTP_DUP == 11) {
-      scan_kind<1>(sc, 0, o2, d, h2, b2); scan_kind<2>(sc, 1, o2, d, h2, b2); scan_kind<3>(sc, 2, o2, d, h2, b2);
-      scan_kind<4>(sc, 3, o2, d, h2, b2); scan_kind<5>(sc, 4, o2, d, h2, b2); scan_kind<6>(sc, 5, o2, d, h2, b2);
+      RTP_SCAN2(1, 0); RTP_SCAN2(2, 1); RTP_SCAN2(3, 2); RTP_SCAN2(4, 3); RTP_SCAN2(5, 4); RTP_SCAN2(6, 5);
     } else if (RTP_DUP == 12) {
-      scan_kind<7>(sc, 6, o2, d, h2, b2); scan_kind<8>(sc, 7, o2, d, h2, b2); scan_kind<9>(sc, 8, o2, d, h2, b2);
+      RTP_SCAN2(7, 6); RTP_SCAN2(8, 7); RTP_SCAN2(9, 8);
     } else if (RTP_DUP == 13) {
-      scan_kind<0>(sc, 10, o2, d, h2, b2);
+      RTP_SCAN2(0, 10);
     } else {
       float t;
       if (sphere_hit(o2, d, tmin, h2.t, ld3(sc->spheres[0].c), sc->spheres[0].rr, t)) h2.t = t;
     }
-    if (__float_as_uint(h2.t) == 0x7fc12345u) h.idx ^= 1;
+    if (__float_as_uint(h2.t) == 0x7fc12345u || (uint32_t)b2 == 0x12345u) h.idx ^= 1;
+#undef RTP_SCAN2
   }
 #endif
   // scan order of the host's grouping: kinds 1..kQuadKinds-1, then 0
+#if RTP_HIT_KEY
+  uint64_t key = kNoHitKey;
+  scan_kind<1>(sc, 0, o, d, key);
+  scan_kind<2>(sc, 1, o, d, key);
+  scan_kind<3>(sc, 2, o, d, key);
+  scan_kind<4>(sc, 3, o, d, key);
+  scan_kind<5>(sc, 4, o, d, key);
+  scan_kind<6>(sc, 5, o, d, key);
+  scan_kind<7>(sc, 6, o, d, key);
+  scan_kind<8>(sc, 7, o, d, key);
+  scan_kind<9>(sc, 8, o, d, key);
+  scan_kind<10>(sc, 9, o, d, key);
+  scan_kind<0>(sc, 10, o, d, key);
+  (void)best;
+  if (key != kNoHitKey) {
+    h.t = __uint_as_float((uint32_t)(key >> 32));
+    h.kind = 0;
+    h.idx = (int)(key & 0xffu);
+  }
+#else
   scan_kind<1>(sc, 0, o, d, h, best);
   scan_kind<2>(sc, 1, o, d, h, best);
   scan_kind<3>(sc, 2, o, d, h, best);
@@ -188,6 +237,7 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d) {
   scan_kind<9>(sc, 8, o, d, h, best);
   scan_kind<10>(sc, 9, o, d, h, best);
   scan_kind<0>(sc, 10, o, d, h, best);
+#endif
   static_assert(kQuadKinds == 11, "closest_hit scans every kind");
   if constexpr (kBvh) {
     spheres_bvh(sc, o, d, h);

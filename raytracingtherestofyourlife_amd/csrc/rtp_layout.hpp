@@ -50,7 +50,8 @@ struct alignas(16) DevQuad {
   int32_t kind;                  // index into kQuadKind
   int32_t orig;                  // index in the reference's quad order (tie-break of equal t)
   int32_t para;                  // e23 == -e01 and e21 == -e03 bit for bit (exact parallelogram)
-  int32_t pad[4];
+  uint32_t key_lo;               // orig << 8 | scan position: low word of the (t, orig) hit key
+  int32_t pad[3];
 };
 
 struct alignas(16) DevSphere {
