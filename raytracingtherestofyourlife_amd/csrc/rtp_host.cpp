@@ -270,7 +270,11 @@ int bvh_build(std::vector<BvhPrim>& P, int b, int e, std::vector<TNode>& T, std:
 }
 
 // threaded flattening for one octant (bit k set: direction component k < 0)
-void bvh_flatten(const std::vector<TNode>& T, int t, int oct, std::vector<rtp::BvhNode>& out) {
+// A one-sphere leaf carries the sphere itself (rtp::kBvhLeafSphere): lo =
+// centre, hi[0] = r*r, hi[1] = the sphere's index (as int bits), so the walk
+// runs the exact root test without a box test or a second dependent load.
+void bvh_flatten(const std::vector<TNode>& T, int t, int oct, const std::vector<int32_t>& order,
+                 const std::vector<rtp::DevSphere>& sph, std::vector<rtp::BvhNode>& out) {
   const int me = (int)out.size();
   out.emplace_back();
   rtp::BvhNode nd{};
@@ -278,11 +282,21 @@ void bvh_flatten(const std::vector<TNode>& T, int t, int oct, std::vector<rtp::B
   std::memcpy(nd.lo, s.lo, sizeof(nd.lo));
   std::memcpy(nd.hi, s.hi, sizeof(nd.hi));
   if (s.left < 0) {
-    nd.leaf = (s.first << 3) | s.count;
+    if (RTP_BVH_EMBED && s.count == 1) {
+      const rtp::DevSphere& S = sph[order[s.first]];
+      std::memcpy(nd.lo, S.c, sizeof(nd.lo));
+      nd.hi[0] = S.rr;
+      int32_t orig = order[s.first];
+      std::memcpy(&nd.hi[1], &orig, sizeof(orig));
+      nd.hi[2] = 0.f;
+      nd.leaf = rtp::kBvhLeafSphere;
+    } else {
+      nd.leaf = (s.first << 3) | s.count;
+    }
   } else {
     const bool neg = (oct >> s.axis) & 1;  // moving toward lower coordinates: right (upper) child first
-    bvh_flatten(T, neg ? s.right : s.left, oct, out);
-    bvh_flatten(T, neg ? s.left : s.right, oct, out);
+    bvh_flatten(T, neg ? s.right : s.left, oct, order, sph, out);
+    bvh_flatten(T, neg ? s.left : s.right, oct, order, sph, out);
     nd.leaf = 0;
   }
   nd.skip = (int32_t)out.size();
@@ -486,7 +500,7 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     bvh_build(P, 0, s->n_spheres, tree, order);
     for (int oct = 0; oct < 8; oct++) {  // 8 copies of n_nodes entries, indices local to each copy
       std::vector<rtp::BvhNode> one;
-      bvh_flatten(tree, 0, oct, one);
+      bvh_flatten(tree, 0, oct, order, sph, one);
       nodes.insert(nodes.end(), one.begin(), one.end());
     }
     geom.resize(order.size());

@@ -134,6 +134,9 @@ RTP_DEV bool sphere_root(f3 o, f3 d, float tmin, f3 c, float rr, float& t_out) {
 // visits spheres in BVH order and keeps that minimum explicitly.  Node boxes
 // only cull (padded on the host; compared with slack here), so no sphere
 // whose root could win is skipped.
+#ifndef RTP_BVH_PREFETCH
+#define RTP_BVH_PREFETCH 1
+#endif
 RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
   const float tmin = 0.001f;
   const float ix = __builtin_amdgcn_rcpf(fabsf(d.x) < 1e-20f ? copysignf(1e-20f, d.x) : d.x);
@@ -142,35 +145,63 @@ RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
   const int nn = sc->n_nodes;
   // the copy of the tree ordered near-to-far for this ray's direction octant
   const int oct = (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0);
-  const BvhNode* __restrict__ nodes = sc->nodes + (int64_t)oct * nn;
+  const float4* __restrict__ nodes = reinterpret_cast<const float4*>(sc->nodes + (int64_t)oct * nn);
   const DevSphereG* __restrict__ geom = sc->sph_geom;
+  auto accept = [&](float t, int orig) {
+    if (t < h.t || (t == h.t && h.kind == 1 && orig < h.idx)) {
+      h.t = t;
+      h.kind = 1;
+      h.idx = orig;
+    }
+  };
   int ni = 0;
+  float4 a = nodes[0], b = nodes[1];
   while (ni < nn) {
-    const float4 a = *reinterpret_cast<const float4*>(&nodes[ni].lo[0]);
-    const float4 b = *reinterpret_cast<const float4*>(&nodes[ni].hi[0]);
-    const float x0 = (a.x - o.x) * ix, x1 = (b.x - o.x) * ix;
-    const float y0 = (a.y - o.y) * iy, y1 = (b.y - o.y) * iy;
-    const float z0 = (a.z - o.z) * iz, z1 = (b.z - o.z) * iz;
-    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
-    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
-    const float slack = 1e-5f * fabsf(tf) + 1e-7f;
-    const bool hit = tn <= tf + slack && tf >= 0.0f && tn <= h.t * 1.00001f + 1e-7f;
+#if RTP_BVH_PREFETCH
+    // node ni+1 (the near child when ni is entered, the next subtree
+    // otherwise) is loaded while ni is tested
+    const int nx = min(ni + 1, nn - 1);
+    const float4 an = nodes[2 * nx], bn = nodes[2 * nx + 1];
+#endif
     const int skip = __float_as_int(a.w), leaf = __float_as_int(b.w);
-    if (hit && leaf) {
-      const int first = leaf >> 3, cnt = leaf & 7;
-      for (int j = first; j < first + cnt; j++) {
-        const float4 g0 = *reinterpret_cast<const float4*>(&geom[j].c[0]);
-        const int orig = geom[j].orig;
-        float t;
-        if (sphere_root(o, d, tmin, mk(g0.x, g0.y, g0.z), g0.w, t) &&
-            (t < h.t || (t == h.t && h.kind == 1 && orig < h.idx))) {
-          h.t = t;
-          h.kind = 1;
-          h.idx = orig;
+    int next;
+    if (leaf == kBvhLeafSphere) {  // one embedded sphere: a.xyz centre, b.x radius^2, b.y index
+      float t;
+      if (sphere_root(o, d, tmin, mk(a.x, a.y, a.z), b.x, t)) accept(t, __float_as_int(b.y));
+      next = skip;
+    } else {
+      const float x0 = (a.x - o.x) * ix, x1 = (b.x - o.x) * ix;
+      const float y0 = (a.y - o.y) * iy, y1 = (b.y - o.y) * iy;
+      const float z0 = (a.z - o.z) * iz, z1 = (b.z - o.z) * iz;
+      const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+      const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+      const float slack = 1e-5f * fabsf(tf) + 1e-7f;
+      const bool hit = tn <= tf + slack && tf >= 0.0f && tn <= h.t * 1.00001f + 1e-7f;
+      if (hit && leaf) {
+        const int first = leaf >> 3, cnt = leaf & 7;
+        for (int j = first; j < first + cnt; j++) {
+          const float4 g0 = *reinterpret_cast<const float4*>(&geom[j].c[0]);
+          float t;
+          if (sphere_root(o, d, tmin, mk(g0.x, g0.y, g0.z), g0.w, t)) accept(t, geom[j].orig);
         }
       }
+      next = (hit && !leaf) ? ni + 1 : skip;
     }
-    ni = (hit && !leaf) ? ni + 1 : skip;
+#if RTP_BVH_PREFETCH
+    if (next == ni + 1) {
+      a = an;
+      b = bn;
+    } else if (next < nn) {
+      a = nodes[2 * next];
+      b = nodes[2 * next + 1];
+    }
+#else
+    if (next < nn) {
+      a = nodes[2 * next];
+      b = nodes[2 * next + 1];
+    }
+#endif
+    ni = next;
   }
 }
 

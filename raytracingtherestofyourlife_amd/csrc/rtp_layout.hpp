@@ -79,8 +79,14 @@ struct alignas(16) BvhNode {
   float lo[3];
   int32_t skip;
   float hi[3];
-  int32_t leaf;  // 0: inner; else (first << 3) | count, count in 1..kBvhLeafSize
+  int32_t leaf;  // 0: inner; kBvhLeafSphere: one embedded sphere; else (first << 3) | count
 };
+// leaf value of a one-sphere leaf that holds the sphere itself: lo = centre,
+// hi[0] = radius^2, hi[1] = sphere index (int bits)
+constexpr int32_t kBvhLeafSphere = -1;
+#ifndef RTP_BVH_EMBED
+#define RTP_BVH_EMBED 1
+#endif
 
 struct alignas(16) DevLights {
   DevQuad quad;   // light quad for QuadPDFWorklet (PdfWorklet.h:230-248)
