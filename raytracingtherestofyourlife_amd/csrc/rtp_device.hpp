@@ -481,10 +481,22 @@ RTP_DEV float sphere_pdf_value(const DevLights& L, f3 o, f3 v) {
 }
 
 // DielectricWorklet (EmitWorklet.h:153-226)
+// pow(x, 5.0) in double.  Inlined, the compiler hoists its ~15 double
+// polynomial constants out of the render loop into ~30 VGPRs held for the
+// whole kernel (and spills around them); as a call they live only in the
+// callee, which runs on dielectric hits alone.
+#ifndef RTP_POW_NOINLINE
+#define RTP_POW_NOINLINE 1
+#endif
+#if RTP_POW_NOINLINE
+__device__ __attribute__((noinline)) double pow5(double x) { return pow(x, 5.0); }
+#else
+RTP_DEV double pow5(double x) { return pow(x, 5.0); }
+#endif
 RTP_DEV float schlick(float cosine, float ref_idx) {
   float r0 = (1 - ref_idx) / (1 + ref_idx);
   r0 = r0 * r0;
-  return (float)(r0 + (1 - r0) * pow((double)(1 - cosine), 5.0));
+  return (float)(r0 + (1 - r0) * pow5((double)(1 - cosine)));
 }
 RTP_DEV void dielectric_scatter(f3 dir, f3 n, float ref_idx, float rnd, f3& sd) {
   f3 reflected = sub(dir, scl(n, 2 * dot(dir, n)));

@@ -157,13 +157,18 @@ RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
   int ni = 0;
   float4 a = nodes[0], b = nodes[1];
   while (ni < nn) {
+    const int skip = __float_as_int(a.w), leaf = __float_as_int(b.w);
 #if RTP_BVH_PREFETCH
-    // node ni+1 (the near child when ni is entered, the next subtree
-    // otherwise) is loaded while ni is tested
+    // node ni+1 (the near child when ni is entered) is loaded while ni is
+    // tested; with RTP_BVH_PREFETCH=2 the skip target too, so either way the
+    // next node is already in flight
     const int nx = min(ni + 1, nn - 1);
     const float4 an = nodes[2 * nx], bn = nodes[2 * nx + 1];
+#if RTP_BVH_PREFETCH >= 2
+    const int sx = min(skip, nn - 1);
+    const float4 as = nodes[2 * sx], bs = nodes[2 * sx + 1];
 #endif
-    const int skip = __float_as_int(a.w), leaf = __float_as_int(b.w);
+#endif
     int next;
     if (leaf == kBvhLeafSphere) {  // one embedded sphere: a.xyz centre, b.x radius^2, b.y index
       float t;
@@ -187,7 +192,10 @@ RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
       }
       next = (hit && !leaf) ? ni + 1 : skip;
     }
-#if RTP_BVH_PREFETCH
+#if RTP_BVH_PREFETCH >= 2
+    a = (next == ni + 1) ? an : as;
+    b = (next == ni + 1) ? bn : bs;
+#elif RTP_BVH_PREFETCH
     if (next == ni + 1) {
       a = an;
       b = bn;
