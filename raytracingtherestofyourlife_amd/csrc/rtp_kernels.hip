@@ -591,9 +591,18 @@ __global__ void __launch_bounds__(256) rtp_render_lockstep(const DevScene* __res
 
 // ------------------------------------------------------------------ v2 ---
 constexpr int kWavesPerBlock = 4;
-constexpr int kPool = 256;  // pixel slots per wave (power of two: queue index = cursor & (kPool-1))
-// LDS per wave: seed, r, g, b, samples, live (u32) + rem, q_ready, q_ff, pad (u16)
-constexpr int kSlotBytes = 6 * 4 + 4 * 2;
+#ifndef RTP_POOL
+#define RTP_POOL 128
+#endif
+constexpr int kPool = RTP_POOL;  // pixel slots per wave (power of two: queue index = cursor & (kPool-1))
+static_assert((kPool & (kPool - 1)) == 0 && kPool >= 64, "pool size must be a power of two >= 64");
+// LDS per wave: seed, r, g, b, samples, live (u32) + rem, q_ready, q_ff (u16):
+// 30 B x 128 slots x 4 waves + the 2 KB quad shading table = 17 KiB per
+// block.  Occupancy is set by VGPRs (5 waves per SIMD at <= 96, below).
+// Measured on C2 / C3 / C4: 128 slots at 5 waves beat 256 slots at 4 waves
+// by 6 / 10 / 5%; 256 slots at 5 waves (LDS booked to the last byte) and
+// 128 slots at 6 waves (80 VGPRs, spills) were slower.
+constexpr int kSlotBytes = 6 * 4 + 3 * 2;
 // s_rem packs the remaining dead depths with how the sample's path ended
 constexpr int kRemMask = 0x3fff, kEndLight = 0x4000, kEndNonfinite = 0x8000;
 constexpr int kPoolLdsBytes = kWavesPerBlock * kPool * kSlotBytes;
@@ -628,10 +637,21 @@ RTP_DEV void set_priority(float lag) {  // s_setprio needs an immediate
 }
 
 #ifndef RTP_POOL_MIN_WAVES_PER_EU
-#define RTP_POOL_MIN_WAVES_PER_EU 4
+#define RTP_POOL_MIN_WAVES_PER_EU 5
+#endif
+// gfx950 allocates VGPRs in granules of 8: 5 waves per SIMD need <= 96.  The
+// waves-per-EU hint alone settles at 102 (4 waves); the hard cap costs one
+// spilled 64-bit value (16 B of scratch).
+#ifndef RTP_POOL_MAX_VGPR
+#define RTP_POOL_MAX_VGPR 96
 #endif
 template <bool kStats, bool kBvh>
-__global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) rtp_render_pool(const DevScene* __restrict__ sc, KParams p, int n_waves) {
+#if RTP_POOL_MAX_VGPR > 0
+#define RTP_POOL_VGPR_ATTR __attribute__((amdgpu_num_vgpr(RTP_POOL_MAX_VGPR)))
+#else
+#define RTP_POOL_VGPR_ATTR
+#endif
+__global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_ATTR rtp_render_pool(const DevScene* __restrict__ sc, KParams p, int n_waves) {
   __shared__ __align__(16) unsigned char smem[kPoolLdsBytes];
   __shared__ float s_qshade[kLdsQuads * kQShadeFloats];
   const int lane = threadIdx.x & 63;
