@@ -14,7 +14,9 @@
 // <raw>-<phi>-<theta>.f32 (hemisphere) for bit-exact comparisons.  -rank/-world shard the hemisphere views (view v
 // goes to rank v mod world; no communication).  -dry-run prints the views
 // (phi, theta, camera position as float bit patterns) and renders nothing.
-// -direct (the AOV mappers) is not on the path tracer's route (out of scope).
+// -direct: the quad mappers' one-bounce AOVs (main.cc:623-651, generate()
+// :399-420): direct.pnm, depth.pnm, normals.pnm, albedo.pnm (or
+// direct-<phi>-<theta>.pnm ... per hemisphere view), all four from one launch.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -68,7 +70,7 @@ uint32_t bits(float f) {
 int main(int argc, char** argv) {
   int x = 128, y = 128, s = 10, depth = 5, variant = 0, device = 0;  // main.cc:56-62 defaults
   int phiCount = 15, thetaCount = 15, rank = 0, world = 1;
-  bool hemi = false, dry = false;
+  bool hemi = false, dry = false, direct = false;
   std::string out = "output", raw;
   for (int i = 1; i < argc; i++) {
     auto next = [&](const char* flag) -> const char* {
@@ -90,10 +92,7 @@ int main(int argc, char** argv) {
     else if ((v = next("-world"))) world = std::atoi(v);
     else if (!std::strcmp(argv[i], "-hemisphere")) hemi = true;
     else if (!std::strcmp(argv[i], "-dry-run")) dry = true;
-    else if (!std::strcmp(argv[i], "-direct")) {
-      std::cerr << argv[i] << ": not part of the path-tracing route (see DESIGN.md, out of scope)\n";
-      return 2;
-    }
+    else if (!std::strcmp(argv[i], "-direct")) direct = true;
   }
   if (world < 1 || rank < 0 || rank >= world || phiCount < 1 || thetaCount < 1) {
     std::cerr << "rtp_path: bad -rank/-world/-phicount/-thetacount" << std::endl;
@@ -118,6 +117,14 @@ int main(int argc, char** argv) {
     rtp::rendering::Camera cam = rtp::DefaultCamera();
     auto dev = std::make_shared<rtp::Device>(device);
     auto render = [&](const std::string& suffix) {  // generate() / the default branch of main()
+      if (direct) {  // runRay + depth, runNorms, runAlbedo (main.cc:399-420, 625-650)
+        const rtp::rendering::DirectBuffers b = rtp::RunDirect(x, y, cam, cb, dev);
+        rtp::SavePNM("direct" + suffix + ".pnm", b.color, x, y);
+        rtp::SaveDepthPNM("depth" + suffix + ".pnm", b.depth, x, y);
+        rtp::SavePNM("normals" + suffix + ".pnm", b.normals, x, y);
+        rtp::SavePNM("albedo" + suffix + ".pnm", b.albedo, x, y);
+        return;
+      }
       rtp::runPath(x, y, s, depth, canvas, cam, cb, dev);
       rtp::SavePNM(out + suffix + ".pnm", canvas);
       if (!raw.empty()) {

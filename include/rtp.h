@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define RTP_ABI_VERSION 1
+#define RTP_ABI_VERSION 2
 
 typedef enum {
   RTP_OK = 0,
@@ -150,6 +150,65 @@ rtp_status rtp_write_pnm(const char* path, const float* rgba, int32_t nx, int32_
  * from the reference's RNG, see oracle/rtp_oracle.h for the exact recipe).
  * The returned descriptor points into library-owned static storage. */
 rtp_status rtp_cornell_box(int32_t variant, rtp_scene_desc* out);
+
+/* ------------------------------------------------------------------------
+ * -direct mode (main.cc:120-251, 623-651; generate() :386-431): the quad
+ * mappers MapperQuad (colour), MapperQuadNormals and MapperQuadAlbedo
+ * (MapperQuad*.cxx:86-150) painted by View3D (View3D.cxx:53-64).  One call
+ * renders any subset of the three AOVs and the canvas depth buffer with one
+ * intersection pass; each output equals the canvas colour buffer of its own
+ * reference render (runRay / runNorms / runAlbedo each start from a cleared
+ * canvas), and depth equals the canvas depth buffer of any of them.  Only
+ * quads are drawn (the mappers use the QuadExtractor alone). */
+typedef enum {
+  RTP_AOV_COLOR = 1,   /* MapperQuad: RayTracer SurfaceColor (Phong over the colour map) */
+  RTP_AOV_NORMALS = 2, /* MapperQuadNormals: RayTracerNormals.cxx:84-141 */
+  RTP_AOV_ALBEDO = 4,  /* MapperQuadAlbedo: RayTracerAlbedo.cxx:84-145 */
+} rtp_aov;
+
+typedef struct {
+  float clip_near, clip_far; /* vtkm::rendering::Camera::SetClippingRange (main.cc:615: 0.1, 5) */
+  float background[4];       /* View3D background colour (main.cc:181: 0,0,0,1) */
+  int32_t composite_background; /* Mapper::SetCompositeBackground (MapperQuad.cxx:46-49: on) */
+  /* per quad, in rtp_scene_desc order: the actor's field at QuadIds[0] (the
+   * cell id) normalised over the scalar range -- QuadIntersector::
+   * IntersectionData's GetScalar; rtp_quad_scalars computes it */
+  const float* quad_scalar;
+  /* Mapper::ColorMap: float4[color_map_size] (Mapper::SetActiveColorTable,
+   * 1024 samples of the actor's colour table; rtp_sample_color_table) */
+  const float* color_map;
+  int32_t color_map_size;
+} rtp_direct_desc;
+
+/* Host buffers (nullable each, at least one non-NULL): rgba float4[nx*ny] per
+ * AOV, depth float[nx*ny].  aovs is informational: an AOV is rendered iff its
+ * buffer is non-NULL.  Synchronous. */
+rtp_status rtp_render_direct(rtp_context* ctx, const rtp_camera* cam, int32_t nx, int32_t ny,
+                             const rtp_direct_desc* desc, float* color_rgba, float* normals_rgba,
+                             float* albedo_rgba, float* depth, rtp_stats* stats);
+/* Same with device buffers on hip_stream (0 = null stream); asynchronous
+ * unless stats != NULL. */
+rtp_status rtp_render_direct_device(rtp_context* ctx, const rtp_camera* cam, int32_t nx, int32_t ny,
+                                    const rtp_direct_desc* desc, float* d_color_rgba, float* d_normals_rgba,
+                                    float* d_albedo_rgba, float* d_depth, void* hip_stream, rtp_stats* stats);
+
+/* Host helpers of the -direct application layer (no device needed). */
+/* vtkm::cont::ColorTable(name, RGB, nanColor, rgbPoints, alphaPoints) sampled
+ * by Mapper::SetActiveColorTable: n_samples float4 colours (uint8 / 255). */
+rtp_status rtp_sample_color_table(const double* rgb_points, int32_t n_rgb, const double* alpha_points,
+                                  int32_t n_alpha, const double nan_color[3], int32_t n_samples, float* out_rgba);
+/* QuadIntersector GetScalar per quad: (field[quad_cell[q]] - min) * invDelta
+ * with min/max over the whole field (Actor::Init's scalar range). */
+rtp_status rtp_quad_scalars(const float* field, int32_t n_field, const int32_t* quad_cell, int32_t n_quads,
+                            float* out);
+/* CornellBox's "point_var" field and the cell id of each quad
+ * (CornellBox.cpp:36-60, 163-418; QuadIds[0]); library-owned storage. */
+rtp_status rtp_cornell_point_field(int32_t variant, const float** field, int32_t* n_field,
+                                   const int32_t** quad_cell, int32_t* n_quads);
+/* save() of a Float32 buffer (main.cc:346-359): NaN -> 0, sqrt, int(255.99*c). */
+rtp_status rtp_write_pnm_depth(const char* path, const float* depth, int32_t nx, int32_t ny);
+/* Diagnostics: the device powf restatement (glibc_powf.hpp) elementwise. */
+rtp_status rtp_eval_powf(rtp_context* ctx, const float* x, float y, float* out, int64_t n);
 
 /* Diagnostics: evaluate a device primitive elementwise (tests only).
  * kind 0: glibc-exact sinf port, 1: cosf port, 2: 1/sqrtf(x) (RMagnitude),

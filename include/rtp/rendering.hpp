@@ -13,6 +13,11 @@
 //   rtp::Normalize(canvas.GetColorBuffer(), spp);       // NormalizeFunctor
 //   rtp::SavePNM("output.pnm", canvas);                  // save(), main.cc:325-384
 //
+// The -direct mode (main.cc:120-251) has the quad mappers MapperQuad,
+// MapperQuadNormals and MapperQuadAlbedo (MapperQuad*.cxx:86-150) with
+// runRay / runNorms / runAlbedo, and RunDirect: all three AOVs + depth from
+// one launch.
+//
 // Reference: MapperPathTracer.h:44-159, MapperPathTracer.cxx:94-406 (ctor,
 // SetCanvas, RenderCells, StartScene/EndScene, NewCopy), main.cc:253-384
 // (NormalizeFunctor, runPath, save), CornellBox.h:9-55.
@@ -23,6 +28,7 @@
 // render throws.
 #pragma once
 
+#include <algorithm>
 #include <array>
 #include <cstdint>
 #include <memory>
@@ -77,9 +83,22 @@ struct CellSet {
 };
 using CoordinateSystem = std::vector<Vec3f>;
 
+// vtkm::cont::Field with point association: one value per entry.
+struct Field {
+  std::string name;
+  std::vector<float> values;
+};
+
 struct DataSet {
   CellSet cells;
+  std::vector<int32_t> quadCells;  // QuadIds[0]: the cell id of each quad
+  std::vector<Field> fields;
   const CellSet& GetCellSet() const { return cells; }
+  const Field& GetField(const std::string& name) const {
+    for (const Field& f : fields)
+      if (f.name == name) return f;
+    throw ErrorBadValue("No field with requested name: " + name);
+  }
 };
 
 // CornellBox (CornellBox.h:9-55): matIdx/texIdx are arrays of two index lists,
@@ -116,6 +135,12 @@ struct CornellBox {
     for (int k = 0; k < 4; k++) lightQuad[k] = d.light_quad_points[k];
     lightSphere = d.light_sphere_point;
     ior = d.ior;
+    const float* fv = nullptr;
+    const int32_t* qc = nullptr;
+    int32_t nf = 0, nq = 0;
+    Check(rtp_cornell_point_field(variant, &fv, &nf, &qc, &nq));
+    ds.quadCells.assign(qc, qc + nq);
+    ds.fields.assign(1, Field{"point_var", std::vector<float>(fv, fv + nf)});  // CornellBox.cpp:411-416
   }
 };
 
@@ -135,6 +160,7 @@ class Camera {
   const Vec3f& GetLookAt() const { return look_at_; }
   const Vec3f& GetViewUp() const { return view_up_; }
   float GetFieldOfView() const { return fov_; }
+  const std::array<float, 2>& GetClippingRange() const { return clip_; }
 
   rtp_camera ToC() const {
     rtp_camera c{};
@@ -166,20 +192,45 @@ class Canvas {
   int width_, height_;
 };
 
-// Colour buffer: Vec4f per pixel, index j*nx + i (row 0 = camera bottom).
+// Colour buffer: Vec4f per pixel, index j*nx + i (row 0 = camera bottom);
+// depth buffer: float per pixel (written by the -direct mappers).
 class CanvasRayTracer : public Canvas {
  public:
-  CanvasRayTracer(int w, int h) : Canvas(w, h), color_((size_t)w * h, Vec4f{0.f, 0.f, 0.f, 0.f}) {}
+  CanvasRayTracer(int w, int h)
+      : Canvas(w, h), color_((size_t)w * h, Vec4f{0.f, 0.f, 0.f, 0.f}), depth_((size_t)w * h, 1.001f) {}
   std::vector<Vec4f>& GetColorBuffer() { return color_; }
   const std::vector<Vec4f>& GetColorBuffer() const { return color_; }
+  std::vector<float>& GetDepthBuffer() { return depth_; }
+  const std::vector<float>& GetDepthBuffer() const { return depth_; }
+  // Canvas::Clear (VTK-m): colour 0, depth 1.001
+  void Clear() {
+    std::fill(color_.begin(), color_.end(), Vec4f{0.f, 0.f, 0.f, 0.f});
+    std::fill(depth_.begin(), depth_.end(), 1.001f);
+  }
 
  private:
   std::vector<Vec4f> color_;
+  std::vector<float> depth_;
 };
 
-struct Field {};       // ignored by the path tracer (MapperPathTracer.cxx:356-383)
-struct ColorTable {};  // ignored
-struct Range {};       // ignored
+using Field = rtp::Field;  // ignored by the path tracer (MapperPathTracer.cxx:356-383)
+
+// vtkm::cont::ColorTable(name, RGB, nanColor, rgbPoints, alphaPoints):
+// (x, r, g, b) and (x, alpha, midpoint, sharpness) quadruples.  Ignored by
+// the path tracer; sampled by the quad mappers (Mapper::SetActiveColorTable).
+struct ColorTable {
+  std::string name;
+  Vec3f nanColor{0.5f, 0.f, 0.f};
+  std::vector<double> rgbPoints, alphaPoints{0.0, 1.0, 0.5, 0.0, 1.0, 1.0, 0.5, 0.0};
+  std::vector<Vec4f> Sample(int n = 1024) const {
+    std::vector<Vec4f> out((size_t)n);
+    const double nanc[3] = {nanColor[0], nanColor[1], nanColor[2]};
+    Check(rtp_sample_color_table(rgbPoints.data(), (int32_t)rgbPoints.size(), alphaPoints.data(),
+                                 (int32_t)alphaPoints.size(), nanc, n, out.data()->data()));
+    return out;
+  }
+};
+struct Range {};  // ignored
 
 // vtkm::rendering::MapperPathTracer.  RenderCells leaves the UN-normalised
 // per-pixel sum over `sc` samples in the canvas colour buffer; normalisation
@@ -284,7 +335,180 @@ class MapperPathTracer {
   float ior_ = 1.5f;
 };
 
+// -direct mode: the quad mappers (MapperQuad*.cxx:86-150).  RenderCells
+// paints the mapper's AOV and the depth into the canvas like View3D::Paint
+// (cleared canvas, background (0,0,0,1) composited).
+inline std::vector<float> QuadScalars(const Field& f, const std::vector<int32_t>& quadCells) {
+  std::vector<float> out(quadCells.size());
+  Check(rtp_quad_scalars(f.values.data(), (int32_t)f.values.size(), quadCells.data(), (int32_t)quadCells.size(),
+                         out.data()));
+  return out;
+}
+
+struct DirectBuffers {
+  std::vector<Vec4f> color, normals, albedo;
+  std::vector<float> depth;
+};
+
+// One rtp_render_direct launch: the AOVs whose bit is set in `aovs`, + depth.
+inline DirectBuffers RenderDirect(rtp_context* ctx, const Camera& camera, int nx, int ny,
+                                  const std::vector<float>& qscalar, const std::vector<Vec4f>& cmap, int aovs,
+                                  const Vec4f& background = {0.f, 0.f, 0.f, 1.f}, bool composite = true) {
+  DirectBuffers b;
+  const size_t n = (size_t)nx * ny;
+  if (aovs & RTP_AOV_COLOR) b.color.resize(n);
+  if (aovs & RTP_AOV_NORMALS) b.normals.resize(n);
+  if (aovs & RTP_AOV_ALBEDO) b.albedo.resize(n);
+  b.depth.resize(n);
+  rtp_direct_desc d{};
+  d.clip_near = camera.GetClippingRange()[0];
+  d.clip_far = camera.GetClippingRange()[1];
+  for (int k = 0; k < 4; k++) d.background[k] = background[k];
+  d.composite_background = composite ? 1 : 0;
+  d.quad_scalar = qscalar.data();
+  d.color_map = cmap.empty() ? nullptr : cmap.data()->data();
+  d.color_map_size = (int32_t)cmap.size();
+  const rtp_camera cam = camera.ToC();
+  auto ptr = [](std::vector<Vec4f>& v) { return v.empty() ? nullptr : v.data()->data(); };
+  Check(rtp_render_direct(ctx, &cam, nx, ny, &d, ptr(b.color), ptr(b.normals), ptr(b.albedo), b.depth.data(),
+                          nullptr));
+  return b;
+}
+
+class MapperQuadBase {
+ public:
+  explicit MapperQuadBase(int aov, std::shared_ptr<Device> device = nullptr) : aov_(aov), device_(std::move(device)) {}
+  virtual ~MapperQuadBase() = default;
+  void SetCanvas(Canvas* canvas) {  // MapperQuad.cxx:65-79
+    if (canvas != nullptr && dynamic_cast<CanvasRayTracer*>(canvas) == nullptr)
+      throw ErrorBadValue("Ray Tracer: bad canvas type. Must be CanvasRayTracer");
+    canvas_ = static_cast<CanvasRayTracer*>(canvas);
+  }
+  Canvas* GetCanvas() const { return canvas_; }
+  void SetCompositeBackground(bool on) { composite_ = on; }
+  void SetBackground(const Vec4f& bg) { background_ = bg; }
+  void SetActiveColorTable(const ColorTable& ct) { colorMap_ = ct.Sample(1024); }  // vtkm Mapper: 1024 samples
+  void StartScene() {}
+  void EndScene() {}
+  // MapperQuad.cxx:86-150 over a scene with quads only (QuadExtractor)
+  void RenderCells(const CellSet& cellset, const CoordinateSystem& coords, const Field& scalarField,
+                   const std::vector<int32_t>& quadCells, const Camera& camera) {
+    if (!canvas_) throw ErrorBadValue("MapperQuad: SetCanvas was not called");
+    const size_t nq = cellset.quads.size();
+    std::vector<int32_t> zq(nq, 0), one(1, 0);
+    std::vector<float> rad(1, 1.f), tex(3, 0.f);
+    rtp_scene_desc d{};
+    d.points = coords.empty() ? nullptr : coords.data()->data();
+    d.n_points = (int32_t)coords.size();
+    d.quad_points = nq ? cellset.quads.data()->data() : nullptr;
+    d.quad_mat = zq.data();
+    d.quad_tex = zq.data();
+    d.n_quads = (int32_t)nq;
+    d.sphere_point = one.data();  // the ABI's light-sphere slot; spheres are not drawn here
+    d.sphere_radius = rad.data();
+    d.sphere_mat = one.data();
+    d.sphere_tex = one.data();
+    d.n_spheres = 1;
+    d.mat_type = one.data();
+    d.n_mat = 1;
+    d.tex_type = one.data();
+    d.n_tex_type = 1;
+    d.tex_rgb = tex.data();
+    d.n_tex = 1;
+    for (int k = 0; k < 4; k++) d.light_quad_points[k] = nq ? cellset.quads[0][k] : 0;
+    d.light_sphere_point = 0;
+    d.ior = 1.5f;
+    Check(rtp_set_scene(device(), &d));
+    const std::vector<float> qs = nq ? QuadScalars(scalarField, quadCells) : std::vector<float>();
+    DirectBuffers b = RenderDirect(device(), camera, canvas_->GetWidth(), canvas_->GetHeight(), qs,
+                                   aov_ == RTP_AOV_COLOR ? colorMap_ : std::vector<Vec4f>(), aov_, background_,
+                                   composite_);
+    canvas_->GetColorBuffer() = aov_ == RTP_AOV_COLOR ? b.color : (aov_ == RTP_AOV_NORMALS ? b.normals : b.albedo);
+    canvas_->GetDepthBuffer() = b.depth;
+  }
+
+ private:
+  rtp_context* device() {
+    if (!device_) device_ = std::make_shared<Device>(0);
+    return device_->get();
+  }
+  int aov_;
+  std::shared_ptr<Device> device_;
+  CanvasRayTracer* canvas_ = nullptr;
+  bool composite_ = true;
+  Vec4f background_{0.f, 0.f, 0.f, 1.f};
+  std::vector<Vec4f> colorMap_;
+};
+struct MapperQuad : MapperQuadBase {  // VTK-m RayTracer colour: Phong over the colour map
+  explicit MapperQuad(std::shared_ptr<Device> d = nullptr) : MapperQuadBase(RTP_AOV_COLOR, std::move(d)) {}
+};
+struct MapperQuadNormals : MapperQuadBase {  // RayTracerNormals.cxx
+  explicit MapperQuadNormals(std::shared_ptr<Device> d = nullptr) : MapperQuadBase(RTP_AOV_NORMALS, std::move(d)) {}
+};
+struct MapperQuadAlbedo : MapperQuadBase {  // RayTracerAlbedo.cxx
+  explicit MapperQuadAlbedo(std::shared_ptr<Device> d = nullptr) : MapperQuadBase(RTP_AOV_ALBEDO, std::move(d)) {}
+};
+
 }  // namespace rendering
+
+// The ct_12_quad colour table of runRay / runAlbedo (main.cc:150-176).
+inline rendering::ColorTable MainPalletColorTable() {
+  const std::vector<double> c1 = {0.65, 0.05, 0.05}, c2 = {0.73, 0.73, 0.73}, c3 = {0.12, 0.45, 0.15};
+  const int num_quads = 12 + 6 + 6;
+  rendering::ColorTable ct;
+  ct.name = "pallet_color_table";
+  ct.nanColor = {0.f, 0.f, 0.f};
+  ct.rgbPoints.insert(ct.rgbPoints.end(), c3.begin(), c3.end());
+  ct.rgbPoints.insert(ct.rgbPoints.end(), c1.begin(), c1.end());
+  ct.rgbPoints.insert(ct.rgbPoints.end(), c2.begin(), c2.end());
+  for (int i = 0; i < num_quads - 3; i++) ct.rgbPoints.insert(ct.rgbPoints.end(), c2.begin(), c2.end());
+  ct.alphaPoints.assign(num_quads, 1.0);
+  return ct;
+}
+
+// runRay / runNorms / runAlbedo (main.cc:120-251): one mapper paints the canvas.
+template <typename M>
+inline void runQuadMapper(rendering::CanvasRayTracer& canvas, const rendering::Camera& cam, const CornellBox& cb,
+                          std::shared_ptr<Device> device = nullptr) {
+  M mapper(std::move(device));
+  mapper.SetCanvas(&canvas);
+  mapper.SetActiveColorTable(MainPalletColorTable());
+  canvas.Clear();  // View3D::Paint
+  mapper.RenderCells(cb.ds.GetCellSet(), cb.coord, cb.ds.GetField("point_var"), cb.ds.quadCells, cam);
+}
+inline void runRay(rendering::CanvasRayTracer& c, const rendering::Camera& cam, const CornellBox& cb,
+                   std::shared_ptr<Device> d = nullptr) {
+  runQuadMapper<rendering::MapperQuad>(c, cam, cb, std::move(d));
+}
+inline void runNorms(rendering::CanvasRayTracer& c, const rendering::Camera& cam, const CornellBox& cb,
+                     std::shared_ptr<Device> d = nullptr) {
+  runQuadMapper<rendering::MapperQuadNormals>(c, cam, cb, std::move(d));
+}
+inline void runAlbedo(rendering::CanvasRayTracer& c, const rendering::Camera& cam, const CornellBox& cb,
+                      std::shared_ptr<Device> d = nullptr) {
+  runQuadMapper<rendering::MapperQuadAlbedo>(c, cam, cb, std::move(d));
+}
+
+// The -direct block of main.cc (:623-651) in one launch: colour, normals,
+// albedo and depth on the Cornell box, each equal to its own mapper render.
+inline rendering::DirectBuffers RunDirect(int nx, int ny, const rendering::Camera& cam, const CornellBox& cb,
+                                          std::shared_ptr<Device> device) {
+  rtp_scene_desc d{};
+  Check(rtp_cornell_box(cb.variant, &d));
+  Check(rtp_set_scene(device->get(), &d));
+  const std::vector<float> qs = rendering::QuadScalars(cb.ds.GetField("point_var"), cb.ds.quadCells);
+  return rendering::RenderDirect(device->get(), cam, nx, ny, qs, MainPalletColorTable().Sample(1024),
+                                 RTP_AOV_COLOR | RTP_AOV_NORMALS | RTP_AOV_ALBEDO);
+}
+
+// save() of a colour buffer (main.cc:325-384)
+inline void SavePNM(const std::string& path, const std::vector<Vec4f>& colors, int nx, int ny) {
+  Check(rtp_write_pnm(path.c_str(), colors.data()->data(), nx, ny));
+}
+// save() of the depth buffer (main.cc:346-359)
+inline void SaveDepthPNM(const std::string& path, const std::vector<float>& depth, int nx, int ny) {
+  Check(rtp_write_pnm_depth(path.c_str(), depth.data(), nx, ny));
+}
 
 // NormalizeFunctor (main.cc:253-287): c = sqrt(deNaN(c) / samplecount), in place.
 inline void Normalize(std::vector<Vec4f>& colors, int samplecount) {

@@ -45,6 +45,8 @@ class Scene(ctypes.Structure):
         ("light_box_pointids", ctypes.c_int32 * 5),
         ("light_sphere_point", ctypes.c_int32),
         ("ior", ctypes.c_float),
+        ("n_field", ctypes.c_int32),
+        ("field", ctypes.c_float * (MAX_POINTS + 16)),
     ]
 
     # numpy views -------------------------------------------------------
@@ -178,3 +180,85 @@ def randf_stream(seed: int, n: int):
     s = ctypes.c_uint32(seed)
     vals = [float(lib().rtpo_randf(ctypes.byref(s))) for _ in range(n)]
     return vals, int(s.value)
+
+
+# ------------------------------------------------------------ -direct mode ---
+class DirectCam(ctypes.Structure):
+    """Mirror of rtpo_direct_cam."""
+
+    _fields_ = [("eye", ctypes.c_float * 3), ("nlook", ctypes.c_float * 3), ("dx", ctypes.c_float * 3),
+                ("dy", ctypes.c_float * 3), ("nx", ctypes.c_int32), ("ny", ctypes.c_int32),
+                ("sub_x0", ctypes.c_int32), ("sub_y0", ctypes.c_int32), ("sub_w", ctypes.c_int32),
+                ("sub_h", ctypes.c_int32), ("vp", ctypes.c_float * 16), ("light", ctypes.c_float * 3),
+                ("view_dir", ctypes.c_float * 3)]
+
+
+AOV_COLOR, AOV_NORMALS, AOV_ALBEDO = 1, 2, 4
+
+# main.cc:120-176: the 24-colour "pallet" handed to ColorTable(name, RGB, nan,
+# rgbPoints, alphaPoints) -- read by VTK-m as (x, r, g, b) quadruples
+_C1, _C2, _C3 = [0.65, 0.05, 0.05], [0.73, 0.73, 0.73], [0.12, 0.45, 0.15]
+MAIN_PALLET = np.array(_C3 + _C1 + _C2 + _C2 * 21, dtype=np.float64)
+MAIN_ALPHA = np.ones(24, dtype=np.float64)
+
+
+def _direct_fns():
+    L = lib()
+    if not hasattr(L, "_direct_ready"):
+        f32p = ctypes.POINTER(ctypes.c_float)
+        d64p = ctypes.POINTER(ctypes.c_double)
+        L.rtpo_direct_setup.argtypes = [ctypes.POINTER(Scene), f32p, f32p, f32p, ctypes.c_float, ctypes.c_float,
+                                        ctypes.c_float, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(DirectCam)]
+        L.rtpo_quad_scalars.argtypes = [ctypes.POINTER(Scene), f32p]
+        L.rtpo_sample_color_table.argtypes = [d64p, ctypes.c_int32, d64p, ctypes.c_int32, d64p, ctypes.c_int32, f32p]
+        L.rtpo_sample_color_table.restype = ctypes.c_int32
+        L.rtpo_render_direct.argtypes = [ctypes.POINTER(Scene), ctypes.POINTER(DirectCam), f32p, f32p, ctypes.c_int32,
+                                         f32p, ctypes.c_int32, ctypes.c_int32, f32p, f32p]
+        L._direct_ready = True
+    return L
+
+
+def direct_setup(scene: Scene, nx: int, ny: int, position=None, look_at=None, view_up=None, fov_y=None,
+                 clip=(0.1, 5.0)) -> DirectCam:
+    c = DEFAULT_CAMERA
+    pos = np.ascontiguousarray(c["position"] if position is None else position, dtype=np.float32)
+    la = np.ascontiguousarray(c["look_at"] if look_at is None else look_at, dtype=np.float32)
+    up = np.ascontiguousarray(c["view_up"] if view_up is None else view_up, dtype=np.float32)
+    fov = float(c["fov_y"] if fov_y is None else fov_y)
+    out = DirectCam()
+    _direct_fns().rtpo_direct_setup(ctypes.byref(scene), _fp(pos), _fp(la), _fp(up), fov, clip[0], clip[1], nx, ny,
+                                    ctypes.byref(out))
+    return out
+
+
+def quad_scalars(scene: Scene) -> np.ndarray:
+    out = np.zeros(scene.n_quads, dtype=np.float32)
+    _direct_fns().rtpo_quad_scalars(ctypes.byref(scene), _fp(out))
+    return out
+
+
+def sample_color_table(rgb_points=MAIN_PALLET, alpha_points=MAIN_ALPHA, n: int = 1024, nan=(0.0, 0.0, 0.0)):
+    rgb = np.ascontiguousarray(rgb_points, dtype=np.float64)
+    al = np.ascontiguousarray(alpha_points, dtype=np.float64)
+    nanc = np.ascontiguousarray(nan, dtype=np.float64)
+    out = np.zeros((n, 4), dtype=np.float32)
+    d64 = ctypes.POINTER(ctypes.c_double)
+    rc = _direct_fns().rtpo_sample_color_table(rgb.ctypes.data_as(d64), rgb.size, al.ctypes.data_as(d64), al.size,
+                                               nanc.ctypes.data_as(d64), n, _fp(out))
+    if rc != 0:
+        raise ValueError("rtpo_sample_color_table: bad arguments")
+    return out
+
+
+def render_direct(scene: Scene, cam: DirectCam, aov: int, cmap=None, qscalar=None, bg=(0, 0, 0, 1),
+                  composite: bool = True):
+    """One -direct mapper render. Returns (rgba[n,4], depth[n])."""
+    cmap = sample_color_table() if cmap is None else np.ascontiguousarray(cmap, dtype=np.float32)
+    qs = quad_scalars(scene) if qscalar is None else np.ascontiguousarray(qscalar, dtype=np.float32)
+    bgv = np.ascontiguousarray(bg, dtype=np.float32)
+    n = cam.nx * cam.ny
+    rgba = np.zeros((n, 4), dtype=np.float32)
+    depth = np.zeros(n, dtype=np.float32)
+    _direct_fns().rtpo_render_direct(ctypes.byref(scene), ctypes.byref(cam), _fp(qs), _fp(cmap), cmap.shape[0],
+                                     _fp(bgv), int(composite), aov, _fp(rgba), _fp(depth))
+    return rgba, depth

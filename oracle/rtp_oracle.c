@@ -336,6 +336,7 @@ static void cb_quad(rtpo_scene* s, int* cell, const float pts[4][3], int divide,
     else
       cb_push_point(s, pts[i][0], pts[i][1], pts[i][2]);
   }
+  for (int i = 0; i < 4; i++) s->field[s->n_field++] = (float)*cell; /* buildQuad :56-59 */
   int q = s->n_quads++;
   s->quad_ids[q][0] = *cell;
   for (int i = 0; i < 4; i++) s->quad_ids[q][1 + i] = base + i;
@@ -386,6 +387,7 @@ void rtpo_cornell_box(int32_t variant, rtpo_scene* s) {
   /* yz_rect x=0 red (:189-200); first point is vec3(0,0,0) undivided */
   set4(p, 0, 0, 0, 0, 555, 0, 0, 555, 555, 0, 0, 555);
   cb_quad(s, &cell, p, 1, 0, 0);
+  s->field[s->n_field++] = 1.0f; /* the red wall pushes a fifth value (:196-200) */
   /* light (:204-215) */
   set4(p, 213, 554, 227, 343, 554, 227, 343, 554, 332, 213, 554, 332);
   cb_quad(s, &cell, p, 1, 3, 3);
@@ -432,11 +434,13 @@ void rtpo_cornell_box(int32_t variant, rtpo_scene* s) {
       }
       s->sphere_point[k] = s->n_points;
       cb_push_point(s, d555(cx), d555(cy), d555(cz));
+      s->field[s->n_field++] = (float)cell++; /* vertex cell (:364 pattern) */
       s->sphere_radius[k] = d555(rad);
       s->sphere_mat[k] = mat;
       s->sphere_tex[k] = tex;
     }
     s->n_spheres = RTPO_C3_SPHERES;
+    for (int i = 0; i < s->n_field; i++) s->field[i] /= (float)s->n_field; /* :389-390 */
     return;
   }
   /* small rotated box (:262-353) incl. the y=333 vertex typo (:327) */
@@ -469,6 +473,7 @@ void rtpo_cornell_box(int32_t variant, rtpo_scene* s) {
   s->sphere_mat[0] = 4;
   s->sphere_tex[0] = 0;
   s->n_spheres = 1;
+  s->field[s->n_field++] = (float)cell; /* vertex cell (:364) */
   cell++;
   /* boxes (:368-386) */
   v3 bc = mk(135, 90, 290);
@@ -482,6 +487,7 @@ void rtpo_cornell_box(int32_t variant, rtpo_scene* s) {
   s->light_box_pointids[4] = 11;
   s->light_sphere_point = 4 * 12;
   s->ior = 1.5f;
+  for (int i = 0; i < s->n_field; i++) s->field[i] /= (float)s->n_field; /* :389-390 */
 }
 
 /* ------------------------------------------------------------ camera --- */
@@ -1137,4 +1143,418 @@ int64_t rtpo_check_sincos_vs_libm(float lo, float hi, uint32_t stride, int64_t* 
   }
   if (checked) *checked = n;
   return bad;
+}
+
+/* ================================================================ -direct ===
+ * main.cc -direct (runRay / runNorms / runAlbedo, :120-251; generate(),
+ * :386-431).  One View3D::Paint (View3D.cxx:53-64) of a quad mapper
+ * (MapperQuad.cxx:86-150): Canvas::Clear, rays from VTK-m's raytracing
+ * Camera, RayTracer::Render (IntersectRays, IntersectionData, SurfaceX::
+ * Shade), CanvasRayTracer::WriteToCanvas, BlendBackground.
+ *
+ * VTK-m pieces restated from VTK-m 1.6's published sources (not vendored in
+ * the reference; version not pinned):
+ *  - Canvas::Clear: colour (0,0,0,0), depth 1.001f;
+ *  - Camera::CreateRaysImpl with image-subset mode ON (boundingBox non-empty;
+ *    the reference's own copy switched it off for the path only,
+ *    Camera.cxx:1069) -> FindSubset, then PerspectiveRayGen; the reference's
+ *    copies of both are Camera.cxx:339-423 and :963-1060;
+ *  - BVH closest hit: distance = MaxDistance (inf) and hitIdx = -1 on a
+ *    miss; quads in index order, tmin = 0 < t < tmax strict;
+ *  - QuadIntersector::IntersectionData: intersection = o + t*d; normal =
+ *    Normalize(TriangleNormal(p0,p1,p2)) flipped against the ray; scalar =
+ *    (field[QuadIds[0]] - min) * invDelta (QuadIds[0] is the cell id);
+ *  - SurfaceColor::Shade writes the shaded colour-map colour; the Normals /
+ *    Albedo variants are the reference's RayTracerNormals.cxx:84-141 and
+ *    RayTracerAlbedo.cxx:84-145;
+ *  - WriteToCanvas (SurfaceConverter): depth = 0.5*(VP*p).z/(VP*p).w + 0.5,
+ *    colour blended over the cleared canvas and clamped to [0,1] with
+ *    std::min/std::max (CPU build: NaN -> 1);
+ *  - Camera view/projection matrices (MatrixHelpers::ViewMatrix,
+ *    Camera3DStruct::CreateProjectionMatrix);
+ *  - ColorTable construction from (x,r,g,b) / (x,a,mid,sharp) quadruples
+ *    (AddPoint: sorted insert, equal x overwrites, out-of-[0,1] colours
+ *    dropped), Sample(n): n float-spaced values over the table range, linear
+ *    RGB interpolation, clamped outside the nodes, std::round(c*255). */
+typedef struct {
+  float m[4][4];
+} dmat4;
+static dmat4 m4_identity(void) {
+  dmat4 r;
+  memset(&r, 0, sizeof(r));
+  for (int i = 0; i < 4; i++) r.m[i][i] = 1.f;
+  return r;
+}
+/* vtkm::MatrixMultiply: product(r,c) = Dot(row r, column c), left to right */
+static dmat4 m4_mul(const dmat4* a, const dmat4* b) {
+  dmat4 r;
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) {
+      float acc = a->m[i][0] * b->m[0][j];
+      acc = acc + a->m[i][1] * b->m[1][j];
+      acc = acc + a->m[i][2] * b->m[2][j];
+      acc = acc + a->m[i][3] * b->m[3][j];
+      r.m[i][j] = acc;
+    }
+  return r;
+}
+static void m4_vec(const float m[16], const float v[4], float out[4]) {
+  for (int i = 0; i < 4; i++) {
+    float acc = m[4 * i + 0] * v[0];
+    acc = acc + m[4 * i + 1] * v[1];
+    acc = acc + m[4 * i + 2] * v[2];
+    acc = acc + m[4 * i + 3] * v[3];
+    out[i] = acc;
+  }
+}
+/* MatrixHelpers::ViewMatrix(position, lookAt, up) */
+static dmat4 view_matrix(v3 position, v3 look_at, v3 up) {
+  v3 view_dir = sub(position, look_at);
+  v3 right = cross(up, view_dir);
+  v3 ru = cross(view_dir, right);
+  view_dir = scl(view_dir, rmag(view_dir));
+  right = scl(right, rmag(right));
+  ru = scl(ru, rmag(ru));
+  dmat4 m = m4_identity();
+  m.m[0][0] = right.x, m.m[0][1] = right.y, m.m[0][2] = right.z;
+  m.m[1][0] = ru.x, m.m[1][1] = ru.y, m.m[1][2] = ru.z;
+  m.m[2][0] = view_dir.x, m.m[2][1] = view_dir.y, m.m[2][2] = view_dir.z;
+  m.m[0][3] = -dot(right, position);
+  m.m[1][3] = -dot(ru, position);
+  m.m[2][3] = -dot(view_dir, position);
+  return m;
+}
+/* Camera3DStruct::CreateProjectionMatrix (zoom 1, no pan) */
+static dmat4 projection_matrix(int32_t w, int32_t h, float fov_deg, float near_plane, float far_plane) {
+  dmat4 m = m4_identity();
+  const float aspect = (float)w / (float)h;
+  float fov_rad = fov_deg * PI_180F;
+  fov_rad = tanf(fov_rad * 0.5f);
+  const float size = near_plane * fov_rad;
+  const float left = -size * aspect, right = size * aspect, bottom = -size, top = size;
+  m.m[0][0] = 2.f * near_plane / (right - left);
+  m.m[1][1] = 2.f * near_plane / (top - bottom);
+  m.m[0][2] = (right + left) / (right - left);
+  m.m[1][2] = (top + bottom) / (top - bottom);
+  m.m[2][2] = -(far_plane + near_plane) / (far_plane - near_plane);
+  m.m[3][2] = -1.f;
+  m.m[2][3] = -(2.f * far_plane * near_plane) / (far_plane - near_plane);
+  m.m[3][3] = 0.f;
+  dmat4 T = m4_identity(), Z = m4_identity(); /* Transform3DTranslate(0,0,0), Transform3DScale(1,1,1) */
+  dmat4 tm = m4_mul(&T, &m);
+  return m4_mul(&Z, &tm);
+}
+static inline float stdmax(float a, float b) { return (a < b) ? b : a; } /* (std::max)(a, b) */
+static inline float stdmin(float a, float b) { return (b < a) ? b : a; } /* (std::min)(a, b) */
+
+void rtpo_direct_setup(const rtpo_scene* sc, const float pos[3], const float look_at[3], const float up_in[3],
+                       float fov_y_deg, float clip_near, float clip_far, int32_t nx, int32_t ny,
+                       rtpo_direct_cam* out) {
+  memset(out, 0, sizeof(*out));
+  /* raytracing::Camera::SetParameters on a fresh camera (500x500, fov 30):
+   * SetUp (normalised if changed), SetFieldOfView, SetHeight, SetWidth
+   * (Camera.cxx:624-637, 641-684, 716-764).  The net FovX is fovY for a
+   * square canvas, else 2*atan(w/h * tan(fovY/2)). */
+  v3 up = ld(up_in);
+  if (!(up.x == 0.f && up.y == 1.f && up.z == 0.f)) up = scl(up, rmag(up));
+  float fov_x = fov_y_deg;
+  if (nx != ny) {
+    const float fovy_rad = fov_y_deg * PI_180F;
+    const float vertical = tanf(0.5f * fovy_rad);
+    const float aspect = (float)nx / (float)ny;
+    const float horizontal = aspect * vertical;
+    const float fovx_rad = 2.0f * atanf(horizontal);
+    fov_x = fovx_rad / PI_180F;
+  }
+  v3 position = ld(pos);
+  v3 look = sub(ld(look_at), position); /* CreateRaysImpl: Look = LookAt - Position, Normalize */
+  look = scl(look, rmag(look));
+  /* PerspectiveRayGen constructor (Camera.cxx:351-392), zoom 1 */
+  const float thx = tanf((fov_x * PI_180F) * .5f);
+  const float thy = tanf((fov_y_deg * PI_180F) * .5f);
+  v3 ru = cross(look, up);
+  ru = scl(ru, rmag(ru));
+  v3 rv = cross(ru, look);
+  rv = scl(rv, rmag(rv));
+  v3 dx = scl(ru, (2 * thx / (float)nx));
+  v3 dy = scl(rv, (2 * thy / (float)ny));
+  const float zoom = 1.f;
+  dx = mk(dx.x / zoom, dx.y / zoom, dx.z / zoom);
+  dy = mk(dy.x / zoom, dy.y / zoom, dy.z / zoom);
+  v3 nlook = scl(look, rmag(look));
+  memcpy(out->eye, &position, 12);
+  memcpy(out->nlook, &nlook, 12);
+  memcpy(out->dx, &dx, 12);
+  memcpy(out->dy, &dy, 12);
+  out->nx = nx, out->ny = ny;
+  /* view-projection of the vtkm::rendering::Camera (raw ViewUp) */
+  dmat4 V = view_matrix(position, ld(look_at), ld(up_in));
+  dmat4 P = projection_matrix(nx, ny, fov_y_deg, clip_near, clip_far);
+  dmat4 VP = m4_mul(&P, &V);
+  memcpy(out->vp, VP.m, sizeof(VP.m));
+  /* shape bounds: union of the quads' AABBs (AABBSurface.h:36-78) */
+  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int q = 0; q < sc->n_quads; q++) {
+    const int32_t* id = sc->quad_ids[q];
+    float mn[3], mx[3];
+    for (int k = 0; k < 3; k++) mn[k] = mx[k] = sc->points[id[1]][k];
+    for (int c = 2; c <= 4; c++)
+      for (int k = 0; k < 3; k++) {
+        mn[k] = stdmin(mn[k], sc->points[id[c]][k]);
+        mx[k] = stdmax(mx[k], sc->points[id[c]][k]);
+      }
+    for (int k = 0; k < 3; k++) {
+      const float eps = stdmax(1e-6f, 1.0e-4f * (mx[k] - mn[k]));
+      mn[k] -= eps;
+      mx[k] += eps;
+      lo[k] = lo[k] < mn[k] ? lo[k] : mn[k];
+      hi[k] = hi[k] > mx[k] ? hi[k] : mx[k];
+    }
+  }
+  /* FindSubset (Camera.cxx:963-1060) */
+  if (sc->n_quads == 0 || (position.x >= lo[0] && position.x <= hi[0] && position.y >= lo[1] &&
+                           position.y <= hi[1] && position.z >= lo[2] && position.z <= hi[2])) {
+    out->sub_x0 = 0, out->sub_y0 = 0, out->sub_w = nx, out->sub_h = ny;
+  } else {
+    float xmin = INFINITY, ymin = INFINITY, zmin = INFINITY, xmax = -INFINITY, ymax = -INFINITY, zmax = -INFINITY;
+    for (int i = 0; i < 2; i++)
+      for (int j = 0; j < 2; j++)
+        for (int k = 0; k < 2; k++) {
+          const float e[4] = {i ? hi[0] : lo[0], j ? hi[1] : lo[1], k ? hi[2] : lo[2], 1.f};
+          float t[4];
+          m4_vec(out->vp, e, t);
+          for (int a = 0; a < 3; a++) t[a] = t[a] / t[3];
+          t[0] = (t[0] * 0.5f + 0.5f) * (float)nx;
+          t[1] = (t[1] * 0.5f + 0.5f) * (float)ny;
+          t[2] = (t[2] * 0.5f + 0.5f);
+          zmin = stdmin(zmin, t[2]);
+          zmax = stdmax(zmax, t[2]);
+          if (t[2] < 0 || t[2] > 1) continue;
+          xmin = stdmin(xmin, t[0]);
+          ymin = stdmin(ymin, t[1]);
+          xmax = stdmax(xmax, t[0]);
+          ymax = stdmax(ymax, t[1]);
+        }
+    xmin -= .001f;
+    xmax += .001f;
+    ymin -= .001f;
+    ymax += .001f;
+    xmin = floorf(stdmin(stdmax(0.f, xmin), (float)nx));
+    xmax = ceilf(stdmin(stdmax(0.f, xmax), (float)nx));
+    ymin = floorf(stdmin(stdmax(0.f, ymin), (float)ny));
+    ymax = ceilf(stdmin(stdmax(0.f, ymax), (float)ny));
+    const int32_t dxp = (int32_t)xmax - (int32_t)xmin, dyp = (int32_t)ymax - (int32_t)ymin;
+    if (zmax < 0 || xmin >= xmax || ymin >= ymax) {
+      out->sub_x0 = 0, out->sub_y0 = 0, out->sub_w = 1, out->sub_h = 1;
+    } else {
+      out->sub_x0 = (int32_t)xmin, out->sub_y0 = (int32_t)ymin, out->sub_w = dxp, out->sub_h = dyp;
+    }
+  }
+  /* SurfaceX::run: light = Position + (2,2,2)*Up; Shade: viewDir normalised */
+  v3 light = add(position, mk(2.f * up.x, 2.f * up.y, 2.f * up.z));
+  v3 vd = sub(position, ld(look_at));
+  vd = scl(vd, rmag(vd));
+  memcpy(out->light, &light, 12);
+  memcpy(out->view_dir, &vd, 12);
+}
+
+void rtpo_quad_scalars(const rtpo_scene* sc, float* out) {
+  /* Actor::Init: scalar range = field min/max (double of the float values);
+   * GetScalar's constructor takes them as float */
+  float mn = INFINITY, mx = -INFINITY;
+  for (int i = 0; i < sc->n_field; i++) {
+    mn = sc->field[i] < mn ? sc->field[i] : mn;
+    mx = sc->field[i] > mx ? sc->field[i] : mx;
+  }
+  const float inv = (mx - mn != 0.f) ? 1.f / (mx - mn) : 1.f / mn;
+  for (int q = 0; q < sc->n_quads; q++) {
+    const int32_t cell = sc->quad_ids[q][0];
+    const float s = (cell >= 0 && cell < sc->n_field) ? sc->field[cell] : 0.f;
+    out[q] = (s - mn) * inv;
+  }
+}
+
+typedef struct {
+  double x;
+  float v[4];
+} ct_node;
+/* ColorTable::AddPoint / AddPointAlpha: sorted insert, an equal x overwrites */
+static int ct_add(ct_node* nodes, int n, double x, const float* v, int nv) {
+  int pos = 0;
+  while (pos < n && nodes[pos].x < x) pos++;
+  if (pos < n && nodes[pos].x == x) {
+    memcpy(nodes[pos].v, v, sizeof(float) * nv);
+    return n;
+  }
+  memmove(nodes + pos + 1, nodes + pos, sizeof(ct_node) * (n - pos));
+  nodes[pos].x = x;
+  memcpy(nodes[pos].v, v, sizeof(float) * nv);
+  return n + 1;
+}
+static float ct_uchar(float t) { return (float)(unsigned char)roundf(t * 255.0f) * (1.0f / 255.0f); }
+
+int32_t rtpo_sample_color_table(const double* rgb, int32_t n_rgb, const double* alpha, int32_t n_alpha,
+                                const double nan_color[3], int32_t n_samples, float* out) {
+  if (n_samples < 2 || n_rgb < 0 || n_alpha < 0) return -1;
+  ct_node cn[256], an[256];
+  int nc = 0, na = 0;
+  double rmin = INFINITY, rmax = -INFINITY;
+  if (n_rgb > 0 && n_rgb % 4 == 0)
+    for (int i = 0; i + 3 < n_rgb && nc < 255; i += 4) {
+      const float v[3] = {(float)rgb[i + 1], (float)rgb[i + 2], (float)rgb[i + 3]};
+      if (v[0] < 0 || v[0] > 1 || v[1] < 0 || v[1] > 1 || v[2] < 0 || v[2] > 1) continue;
+      nc = ct_add(cn, nc, rgb[i], v, 3);
+      rmin = rgb[i] < rmin ? rgb[i] : rmin;
+      rmax = rgb[i] > rmax ? rgb[i] : rmax;
+    }
+  if (n_alpha > 0 && n_alpha % 4 == 0)
+    for (int i = 0; i + 3 < n_alpha && na < 255; i += 4) {
+      const float v[3] = {(float)alpha[i + 1], (float)alpha[i + 2], (float)alpha[i + 3]};
+      if (v[0] < 0 || v[0] > 1 || v[1] < 0 || v[1] > 1 || v[2] < 0 || v[2] > 1) continue;
+      na = ct_add(an, na, alpha[i], v, 3);
+      rmin = alpha[i] < rmin ? alpha[i] : rmin;
+      rmax = alpha[i] > rmax ? alpha[i] : rmax;
+    }
+  if (nc == 0 && na == 0) rmin = rmax = 0;
+  const double d_samples = (double)(n_samples - 1);
+  const double d_delta = (rmax - rmin) / d_samples;
+  const float f_samples = (float)(n_samples - 1);
+  const float f_start = (float)rmin;
+  const float f_delta = (float)(rmax - rmin) / f_samples;
+  const float f_end = f_start + (f_delta * f_samples);
+  const int use_f = fabs((double)f_end - rmax) <= 0.002 && fabs((double)f_delta - d_delta) <= 0.002;
+  for (int i = 0; i < n_samples; i++) {
+    double x;
+    if (use_f)
+      x = (double)(i == 0 ? f_start : (i == n_samples - 1 ? f_end : f_start + ((float)i * f_delta)));
+    else
+      x = i == 0 ? rmin : (i == n_samples - 1 ? rmax : rmin + ((double)i * d_delta));
+    float c[3];
+    if (x != x) {
+      for (int k = 0; k < 3; k++) c[k] = (float)nan_color[k];
+    } else if (nc == 0) {
+      c[0] = c[1] = c[2] = 0.f;
+    } else if (x <= cn[0].x) {
+      memcpy(c, cn[0].v, 12);
+    } else if (x >= cn[nc - 1].x) {
+      memcpy(c, cn[nc - 1].v, 12);
+    } else {
+      int s = 1;
+      while (cn[s].x < x) s++;
+      const int f = s - 1;
+      const float w = (float)((x - cn[f].x) / (cn[s].x - cn[f].x));
+      for (int k = 0; k < 3; k++) c[k] = (1.0f - w) * cn[f].v[k] + w * cn[s].v[k]; /* vtkm::Lerp */
+    }
+    float a;
+    if (na == 0) {
+      a = 1.f;
+    } else if (x <= an[0].x) {
+      a = an[0].v[0];
+    } else if (x >= an[na - 1].x) {
+      a = an[na - 1].v[0];
+    } else { /* linear between opacity nodes (midpoint 0.5, sharpness 0 only) */
+      int s = 1;
+      while (an[s].x < x) s++;
+      const int f = s - 1;
+      const float w = (float)((x - an[f].x) / (an[s].x - an[f].x));
+      a = (1.0f - w) * an[f].v[0] + w * an[s].v[0];
+    }
+    out[4 * i + 0] = ct_uchar(c[0]);
+    out[4 * i + 1] = ct_uchar(c[1]);
+    out[4 * i + 2] = ct_uchar(c[2]);
+    out[4 * i + 3] = ct_uchar(a);
+  }
+  return 0;
+}
+
+void rtpo_render_direct(const rtpo_scene* sc, const rtpo_direct_cam* cam, const float* quad_scalar,
+                        const float* cmap, int32_t cmap_n, const float bg[4], int32_t composite, int32_t aov,
+                        float* out_rgba, float* out_depth) {
+  const int32_t nx = cam->nx, ny = cam->ny;
+  const v3 eye = ld(cam->eye), nlook = ld(cam->nlook), ddx = ld(cam->dx), ddy = ld(cam->dy);
+  const v3 L = ld(cam->light), V = ld(cam->view_dir);
+#pragma omp parallel for schedule(static)
+  for (int64_t idx = 0; idx < (int64_t)nx * ny; idx++) {
+    const int32_t i = (int32_t)(idx % nx), j = (int32_t)(idx / nx);
+    float c[4] = {0.f, 0.f, 0.f, 0.f}; /* Canvas::Clear */
+    float depth = 1.001f;
+    if (i >= cam->sub_x0 && i < cam->sub_x0 + cam->sub_w && j >= cam->sub_y0 && j < cam->sub_y0 + cam->sub_h) {
+      /* PerspectiveRayGen::operator() (Camera.cxx:394-421) */
+      v3 rd = add(add(nlook, scl(ddx, ((2.f * (float)i - (float)nx) / 2.0f))),
+                  scl(ddy, ((2.f * (float)j - (float)ny) / 2.0f)));
+      if (rd.x == 0.f) rd.x += 0.0000001f;
+      if (rd.y == 0.f) rd.y += 0.0000001f;
+      if (rd.z == 0.f) rd.z += 0.0000001f;
+      const float sq_mag = sqrtf(dot(rd, rd));
+      const v3 d = mk(rd.x / sq_mag, rd.y / sq_mag, rd.z / sq_mag);
+      /* closest quad hit, index order, 0 < t < tmax */
+      int hq = -1;
+      float closest = INFINITY;
+      for (int q = 0; q < sc->n_quads; q++) {
+        const int32_t* id = sc->quad_ids[q];
+        float T;
+        if (quad_hit(eye, d, ld(sc->points[id[1]]), ld(sc->points[id[2]]), ld(sc->points[id[3]]),
+                     ld(sc->points[id[4]]), &T) &&
+            T < closest && T > 0.f) {
+          closest = T;
+          hq = q;
+        }
+      }
+      float rc[4] = {0.f, 0.f, 0.f, 0.f}; /* Rays.Buffers[0].InitConst(0) */
+      const float dist = closest;          /* MaxDistance (inf) on a miss */
+      if (hq >= 0) {
+        const int32_t* id = sc->quad_ids[hq];
+        const v3 p = add(eye, scl(d, dist));
+        v3 n = cross(sub(ld(sc->points[id[2]]), ld(sc->points[id[1]])), sub(ld(sc->points[id[3]]), ld(sc->points[id[1]])));
+        n = scl(n, rmag(n));
+        if (dot(n, d) > 0.f) n = neg(n);
+        v3 ldir = sub(L, p);
+        ldir = scl(ldir, rmag(ldir));
+        float cos_t = dot(n, ldir);
+        cos_t = stdmin(stdmax(cos_t, 0.f), 1.f);
+        v3 refl = sub(scl(n, 2.f * dot(ldir, n)), ldir);
+        refl = scl(refl, rmag(refl));
+        const float cos_p = dot(refl, V);
+        if (aov == RTPO_AOV_COLOR) {
+          const float spec = powf(stdmax(cos_p, 0.f), 20.f);
+          const float sf = quad_scalar[hq] * (float)(cmap_n - 1);
+          int32_t ci = (sf > -2147483649.0f && sf < 2147483648.0f) ? (int32_t)sf : INT32_MIN; /* cvttss2si */
+          ci = ci > 0 ? ci : 0;
+          ci = ci < cmap_n - 1 ? ci : cmap_n - 1;
+          for (int k = 0; k < 4; k++) rc[k] = cmap[4 * ci + k];
+          for (int k = 0; k < 3; k++) rc[k] *= stdmin(0.5f + 0.7f * cos_t + 0.7f * spec, 1.f);
+        } else if (aov == RTPO_AOV_NORMALS) {
+          rc[0] = n.x, rc[1] = n.y, rc[2] = n.z, rc[3] = 1.0f;
+        } else {
+          rc[0] = (cos_p * refl.x) / (cos_t * ldir.x);
+          rc[1] = (cos_p * refl.y) / (cos_t * ldir.y);
+          rc[2] = (cos_p * refl.z) / (cos_t * ldir.z);
+          rc[3] = 1.0f;
+        }
+      }
+      /* WriteToCanvas / SurfaceConverter */
+      const v3 ip = add(eye, scl(d, dist));
+      const float pt[4] = {ip.x, ip.y, ip.z, 1.f};
+      float np[4];
+      m4_vec(cam->vp, pt, np);
+      const float z = np[2] / np[3];
+      depth = 0.5f * z + 0.5f;
+      const float a = 1.f - rc[3];
+      float o[4];
+      o[0] = rc[0] + c[0] * a;
+      o[1] = rc[1] + c[1] * a;
+      o[2] = rc[2] + c[2] * a;
+      o[3] = c[3] * a + rc[3];
+      for (int k = 0; k < 4; k++) c[k] = stdmin(1.f, stdmax(o[k], 0.f));
+    }
+    if (composite && !(c[3] >= 1.f)) { /* BlendBackground */
+      const float a = bg[3] * (1.f - c[3]);
+      c[0] = c[0] + bg[0] * a;
+      c[1] = c[1] + bg[1] * a;
+      c[2] = c[2] + bg[2] * a;
+      c[3] = a + c[3];
+    }
+    memcpy(out_rgba + 4 * idx, c, 16);
+    if (out_depth) out_depth[idx] = depth;
+  }
 }

@@ -55,6 +55,12 @@ typedef struct {
   int32_t light_box_pointids[5]; /* (0,8,9,10,11) MapperPathTracer.cxx:141 */
   int32_t light_sphere_point;    /* 48, MapperPathTracer.cxx:145 */
   float ior;                     /* 1.5, MapperPathTracer.cxx:467 */
+  /* the "point_var" point field (CornellBox.cpp:36-60, 163-418): each cell
+   * pushes its cell index once per point it adds (the red wall five times,
+   * :189-200), then every value is divided by the value count (:389-390).
+   * Read by the -direct mappers only. */
+  int32_t n_field;
+  float field[RTPO_MAX_POINTS + 16];
 } rtpo_scene;
 
 /* Camera constants shared by every RayGen invocation:
@@ -103,6 +109,45 @@ void rtpo_render_pixels(const rtpo_scene* sc, const float cam[12], int32_t nx, i
 int32_t rtpo_render_soa(const rtpo_scene* sc, const float cam[12], int32_t nx, int32_t ny, int32_t spp,
                         int32_t depth, uint32_t seed_base, int32_t row_begin, int32_t row_end,
                         float* out_rgba, uint32_t* out_seed, uint32_t* out_live, int32_t nthreads);
+
+/* ---------------------------------------------------------------------
+ * -direct mode (main.cc:120-251, 623-651; generate() :386-431): the
+ * MapperQuad / MapperQuadNormals / MapperQuadAlbedo one-bounce renders of
+ * the quads (QuadExtractor: the sphere's vertex cell is not drawn).  One call
+ * is one View3D::Paint: Canvas::Clear, camera rays of VTK-m's raytracing
+ * Camera (PerspectiveRayGen over the FindSubset pixel rectangle), closest hit,
+ * QuadIntersector::IntersectionData, the SurfaceX::Shade of the mapper,
+ * CanvasRayTracer::WriteToCanvas (depth + blend + clamp), BlendBackground.
+ * VTK-m pieces not present in the reference are restated from VTK-m 1.6's
+ * published behaviour ("direct mode"): parity unpinned there. */
+typedef struct {
+  float eye[3], nlook[3], dx[3], dy[3]; /* PerspectiveRayGen (Camera.cxx:339-392) */
+  int32_t nx, ny;
+  int32_t sub_x0, sub_y0, sub_w, sub_h; /* FindSubset pixel rectangle (Camera.cxx:963-1060) */
+  float vp[16];                         /* projection * view, row-major (WriteToCanvas) */
+  float light[3];                       /* Position + (2,2,2)*Up (RayTracerNormals.cxx:155-156) */
+  float view_dir[3];                    /* Normalize(Position - LookAt) */
+} rtpo_direct_cam;
+
+#define RTPO_AOV_COLOR 1
+#define RTPO_AOV_NORMALS 2
+#define RTPO_AOV_ALBEDO 4
+
+void rtpo_direct_setup(const rtpo_scene* sc, const float pos[3], const float look_at[3], const float up[3],
+                       float fov_y_deg, float clip_near, float clip_far, int32_t nx, int32_t ny,
+                       rtpo_direct_cam* out);
+/* QuadIntersector GetScalar per quad: (field[cellId] - min) * invDelta over
+ * the actor's scalar range (min/max of the whole field) */
+void rtpo_quad_scalars(const rtpo_scene* sc, float* out);
+/* ColorTable(name, RGB, nanColor, rgbPoints, alphaPoints) + Mapper::
+ * SetActiveColorTable's Sample(n) into Vec4ui_8 and *(1/255.f) */
+int32_t rtpo_sample_color_table(const double* rgb_points, int32_t n_rgb, const double* alpha_points,
+                                int32_t n_alpha, const double nan_color[3], int32_t n_samples, float* out_rgba);
+/* One mapper render into out_rgba (float4 per pixel) and out_depth
+ * (nullable); aov is one RTPO_AOV_* flag. */
+void rtpo_render_direct(const rtpo_scene* sc, const rtpo_direct_cam* cam, const float* quad_scalar,
+                        const float* cmap, int32_t cmap_n, const float bg[4], int32_t composite, int32_t aov,
+                        float* out_rgba, float* out_depth);
 
 /* NormalizeFunctor (main.cc:253-287): de-NaN rgb, then sqrt(x / spp). */
 void rtpo_normalize(float* rgba, int64_t n, int32_t spp);

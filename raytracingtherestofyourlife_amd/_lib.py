@@ -51,10 +51,21 @@ class RtpPixelAux(ctypes.Structure):
     _fields_ = [("final_seed", u32p), ("live_bounces", u32p)]
 
 
+class RtpDirectDesc(ctypes.Structure):
+    _fields_ = [("clip_near", ctypes.c_float), ("clip_far", ctypes.c_float), ("background", ctypes.c_float * 4),
+                ("composite_background", ctypes.c_int32), ("quad_scalar", f32p), ("color_map", f32p),
+                ("color_map_size", ctypes.c_int32)]
+
+
+RTP_AOV_COLOR, RTP_AOV_NORMALS, RTP_AOV_ALBEDO = 1, 2, 4
+
+
 EXPORTED_SYMBOLS = [
     "rtp_last_error", "rtp_abi_version", "rtp_create", "rtp_destroy", "rtp_set_scene", "rtp_render",
     "rtp_render_device", "rtp_render_pixels", "rtp_normalize", "rtp_write_pnm", "rtp_cornell_box",
     "rtp_eval_primitive", "rtp_debug_counters", "rtp_verify_fast_math",
+    "rtp_render_direct", "rtp_render_direct_device", "rtp_sample_color_table", "rtp_quad_scalars",
+    "rtp_cornell_point_field", "rtp_write_pnm_depth", "rtp_eval_powf",
 ]
 
 
@@ -109,6 +120,18 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.rtp_debug_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32]
     L.rtp_verify_fast_math.argtypes = [vp, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32,
                                        ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]
+    d64p = ctypes.POINTER(ctypes.c_double)
+    L.rtp_render_direct.argtypes = [vp, ctypes.POINTER(RtpCamera), ctypes.c_int32, ctypes.c_int32,
+                                    ctypes.POINTER(RtpDirectDesc), f32p, f32p, f32p, f32p, ctypes.POINTER(RtpStats)]
+    L.rtp_render_direct_device.argtypes = [vp, ctypes.POINTER(RtpCamera), ctypes.c_int32, ctypes.c_int32,
+                                           ctypes.POINTER(RtpDirectDesc), vp, vp, vp, vp, vp,
+                                           ctypes.POINTER(RtpStats)]
+    L.rtp_sample_color_table.argtypes = [d64p, ctypes.c_int32, d64p, ctypes.c_int32, d64p, ctypes.c_int32, f32p]
+    L.rtp_quad_scalars.argtypes = [f32p, ctypes.c_int32, i32p, ctypes.c_int32, f32p]
+    L.rtp_cornell_point_field.argtypes = [ctypes.c_int32, ctypes.POINTER(f32p), ctypes.POINTER(ctypes.c_int32),
+                                          ctypes.POINTER(i32p), ctypes.POINTER(ctypes.c_int32)]
+    L.rtp_write_pnm_depth.argtypes = [ctypes.c_char_p, f32p, ctypes.c_int32, ctypes.c_int32]
+    L.rtp_eval_powf.argtypes = [vp, f32p, ctypes.c_float, f32p, ctypes.c_int64]
     for name in EXPORTED_SYMBOLS:
         if name not in ("rtp_last_error", "rtp_abi_version", "rtp_destroy"):
             getattr(L, name).restype = ctypes.c_int32

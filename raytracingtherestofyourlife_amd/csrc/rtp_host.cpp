@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/rtp.h"
+#include "rtp_context.hpp"
 #include "rtp_layout.hpp"
 
 extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int bvh, int* variant_out, int* waves_out);
@@ -305,28 +306,8 @@ void bvh_flatten(const std::vector<TNode>& T, int t, int oct, const std::vector<
 
 }  // namespace
 
-struct rtp_context {
-  int device = 0;
-  rtp::DevScene* d_scene = nullptr;
-  bool has_scene = false;
-  float* d_hist = nullptr;
-  size_t hist_bytes = 0;
-  unsigned long long* d_dbg = nullptr;  // RTP_DEBUG_STATS=1: per-wave counters of the last launch
-  int dbg_waves = 0;
-  unsigned long long* d_progress = nullptr;  // global finished-sample counter of the pool kernel
-  // many-sphere scenes: threaded BVH + sphere records (rtp_layout.hpp)
-  rtp::BvhNode* d_nodes = nullptr;
-  rtp::DevSphereG* d_sph_geom = nullptr;
-  rtp::DevSphere* d_sph_all = nullptr;
-  bool use_bvh = false;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  // Completion of the last launch.  The history buffer and the progress
-  // counter are per-context scratch, so a launch on any stream first waits
-  // for the previous one, and the host waits before it frees or rewrites a
-  // buffer a queued kernel may still read.
-  hipEvent_t done = nullptr;
-  bool pending = false;
-};
+// error reporting for the other translation units of librtp.so
+rtp_status rtp_internal_fail(rtp_status st, const std::string& msg) { return fail(st, msg); }
 
 namespace {
 rtp_status drain(rtp_context* c) {
@@ -385,6 +366,7 @@ void rtp_destroy(rtp_context* c) {
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->done) (void)hipEventDestroy(c->done);
+  if (c->d_direct) (void)hipFree(c->d_direct);
   delete c;
 }
 
@@ -463,6 +445,29 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     h->kind_begin[rtp::kQuadKinds] = pos;
   }
   h->n_quads = (int32_t)kept.size();
+  // the -direct mode's inputs: kept quad -> reference index, and the shape
+  // bounds (union of the quads' padded AABBs, AABBSurface.h:36-78)
+  std::vector<int32_t> kept_ref(kept.begin(), kept.end());
+  float blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int q = 0; q < s->n_quads; q++) {
+    const int32_t* id = s->quad_points + 4 * q;
+    float mn[3], mx[3];
+    for (int k = 0; k < 3; k++) mn[k] = mx[k] = s->points[3 * id[0] + k];
+    for (int c2 = 1; c2 < 4; c2++)
+      for (int k = 0; k < 3; k++) {
+        const float v = s->points[3 * id[c2] + k];
+        mn[k] = (v < mn[k]) ? v : mn[k];  // vtkm::Min / Max: (std::min)/(std::max)
+        mx[k] = (mx[k] < v) ? v : mx[k];
+      }
+    for (int k = 0; k < 3; k++) {
+      const float ext = 1.0e-4f * (mx[k] - mn[k]);
+      const float eps = (1e-6f < ext) ? ext : 1e-6f;
+      mn[k] -= eps;
+      mx[k] += eps;
+      blo[k] = std::min(blo[k], mn[k]);
+      bhi[k] = std::max(bhi[k], mx[k]);
+    }
+  }
   std::vector<rtp::DevSphere> sph(s->n_spheres);
   for (int k = 0; k < s->n_spheres; k++) {
     if (!pt_ok(s->sphere_point[k]) || !mat_ok(s->sphere_mat[k]) || !tex_ok(s->sphere_tex[k]) ||
@@ -574,6 +579,9 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
   delete h;
   c->use_bvh = use_bvh;
   if (e != hipSuccess) return hip_fail(e, "rtp_set_scene upload");
+  c->kept_quads = std::move(kept_ref);
+  c->n_ref_quads = s->n_quads;
+  for (int k = 0; k < 3; k++) c->quad_lo[k] = blo[k], c->quad_hi[k] = bhi[k];
   c->has_scene = true;
   return RTP_OK;
 }

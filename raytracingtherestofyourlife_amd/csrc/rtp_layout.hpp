@@ -143,6 +143,28 @@ struct KParams {
   const uint32_t* ff[kFfTables];
 };
 
+// -direct mode (main.cc:120-251): one launch renders the requested AOVs of
+// the quad mappers (MapperQuad colour, MapperQuadNormals, MapperQuadAlbedo)
+// and the canvas depth, one lane per pixel of the canvas.
+struct DirectParams {
+  float eye[3], nlook[3], dx[3], dy[3];  // PerspectiveRayGen (Camera.cxx:351-392)
+  int32_t nx, ny;
+  int32_t sub_x0, sub_y0, sub_w, sub_h;  // FindSubset pixel rectangle (Camera.cxx:963-1060)
+  float vp[16];                          // projection * view, row-major (WriteToCanvas)
+  float light[3];                        // Position + (2,2,2)*Up
+  float view_dir[3];                     // Normalize(Position - LookAt)
+  float bg[4];                           // background colour (BlendBackground)
+  int32_t composite;                     // CompositeBackground
+  int32_t cmap_n;                        // colour-map entries
+  const float* qscalar;                  // normalised scalar per kept quad (DevQuad::orig order)
+  const float* cmap;                     // float4[cmap_n]
+  float* color;                          // float4 per pixel (nullable)
+  float* normals;                        // float4 per pixel (nullable)
+  float* albedo;                         // float4 per pixel (nullable)
+  float* depth;                          // float per pixel (nullable)
+  int64_t npix;                          // nx * ny
+};
+
 // per-wave diagnostic counters of the pool kernel (RTP_DEBUG_STATS=1)
 enum DbgCounter {
   kDbgBounceSteps = 0,   // loop iterations that ran a bounce

@@ -28,6 +28,12 @@ struct SceneStore {
   float tex_rgb[12] = {(float)0.65, (float)0.05, (float)0.05, (float)0.73, (float)0.73, (float)0.73,
                        (float)0.12, (float)0.45, (float)0.15, 15.f,         15.f,         15.f};
 
+  // the "point_var" field (CornellBox.cpp:36-60): each cell pushes its cell
+  // index once per point it adds; QuadIds[0] (the cell id) per quad
+  std::vector<float> field;
+  std::vector<int32_t> quad_cell;
+  int cell = 0;
+
   void add_quad(const float p[4][3], int mat, int tex) {
     const int base = (int)(points.size() / 3);
     for (int i = 0; i < 4; i++)
@@ -35,6 +41,13 @@ struct SceneStore {
     for (int i = 0; i < 4; i++) quad_points.push_back(base + i);
     quad_mat.push_back(mat);
     quad_tex.push_back(tex);
+    for (int i = 0; i < 4; i++) field.push_back((float)cell);
+    quad_cell.push_back(cell++);
+  }
+  void add_vertex_cell() { field.push_back((float)cell++); }  // sphere vertex cell (:357-365)
+  void finish_field() {                                       // val /= float(vecField.size()) (:389-390)
+    const float n = (float)field.size();
+    for (float& v : field) v /= n;
   }
 };
 
@@ -111,6 +124,7 @@ void build(SceneStore& s, int variant) {
   s.add_quad(p, 2, 2);
   rect(p, {0, 0, 0, 0, 555, 0, 0, 555, 555, 0, 0, 555});  // red wall (:189-200)
   s.add_quad(p, 0, 0);
+  s.field.push_back(1.f);  // the red wall pushes a fifth field value (:196-200)
   rect(p, {213, 554, 227, 343, 554, 227, 343, 554, 332, 213, 554, 332});  // light (:204-215)
   s.add_quad(p, 3, 3);
   rect(p, {0, 555, 0, 555, 555, 0, 555, 555, 555, 0, 555, 555});  // ceiling
@@ -147,7 +161,9 @@ void build(SceneStore& s, int variant) {
       s.sphere_radius.push_back((float)((double)rad / 555.0));
       s.sphere_mat.push_back(mat);
       s.sphere_tex.push_back(tex);
+      s.add_vertex_cell();
     }
+    s.finish_field();
     return;
   }
   const std::initializer_list<float> small_box[6] = {
@@ -168,12 +184,14 @@ void build(SceneStore& s, int variant) {
   s.sphere_radius.push_back((float)(90 / 555.0));
   s.sphere_mat.push_back(4);
   s.sphere_tex.push_back(0);
+  s.add_vertex_cell();
   const float rad = 90;
   const float bc[3] = {135, 90, 290};
   const float n1[3] = {bc[0] - rad, 0, bc[2] - rad}, f1[3] = {bc[0] + rad, 180, bc[2] + rad};
   box(s, n1, f1);
   const float n2[3] = {50, 0, 50}, f2[3] = {450, 100, 100};
   box(s, n2, f2);
+  s.finish_field();
 }
 
 SceneStore g_store[4];
@@ -210,5 +228,17 @@ extern "C" rtp_status rtp_cornell_box(int32_t variant, rtp_scene_desc* out) {
   out->light_quad_points[3] = 11;
   out->light_sphere_point = s.sphere_point[0];  // 4 * 12 for variants 0..2
   out->ior = 1.5f;
+  return RTP_OK;
+}
+
+extern "C" rtp_status rtp_cornell_point_field(int32_t variant, const float** field, int32_t* n_field,
+                                              const int32_t** quad_cell, int32_t* n_quads) {
+  if (!field || !n_field || !quad_cell || !n_quads || variant < 0 || variant > 3) return RTP_ERR_INVALID_ARGUMENT;
+  std::call_once(g_once[variant], [variant] { build(g_store[variant], variant); });
+  const SceneStore& s = g_store[variant];
+  *field = s.field.data();
+  *n_field = (int32_t)s.field.size();
+  *quad_cell = s.quad_cell.data();
+  *n_quads = (int32_t)s.quad_cell.size();
   return RTP_OK;
 }

@@ -112,9 +112,14 @@ class CanvasRayTracer(Canvas):
     def __init__(self, nx: int, ny: int):
         super().__init__(nx, ny)
         self.color = np.zeros((self.width * self.height, 4), dtype=np.float32)
+        self.depth = np.full(self.width * self.height, np.float32(1.001), dtype=np.float32)
 
     def GetColorBuffer(self) -> np.ndarray:
         return self.color
+
+    def GetDepthBuffer(self) -> np.ndarray:
+        """Canvas depth (written by the -direct mappers; 1.001 = cleared)."""
+        return self.depth
 
 
 # -------------------------------------------------------------- scene --
@@ -125,15 +130,39 @@ class CellSet:
 
     quad_points: np.ndarray  # int32 [Q,4]
     sphere_points: np.ndarray  # int32 [S]
+    quad_cells: np.ndarray | None = None  # int32 [Q]: QuadIds[0], the cell id of each quad
+
+
+@dataclass
+class Field:
+    """vtkm::cont::Field (point association): a name and one value per entry."""
+
+    name: str
+    values: np.ndarray  # float32
+
+    def GetName(self) -> str:
+        return self.name
+
+    def GetRange(self) -> tuple[float, float]:
+        return float(self.values.min()), float(self.values.max())
 
 
 @dataclass
 class DataSet:
     cellset: CellSet
     coords: np.ndarray  # float32 [P,3]
+    fields: dict = field(default_factory=dict)
 
     def GetCellSet(self) -> CellSet:
         return self.cellset
+
+    def GetField(self, name: str) -> Field:
+        if name not in self.fields:
+            raise ErrorBadValue(f"No field with requested name: {name}")
+        return self.fields[name]
+
+    def AddField(self, f: Field) -> None:
+        self.fields[f.name] = f
 
 
 @dataclass
@@ -171,7 +200,12 @@ class CornellBox:
         self.light_quad_points = tuple(int(v) for v in d.light_quad_points)
         self.light_sphere_point = int(d.light_sphere_point)
         self.ior = float(d.ior)
-        self.ds = DataSet(CellSet(quads, spheres), self.coord)
+        fp, nf, qc, nq = _lib.f32p(), ctypes.c_int32(), _lib.i32p(), ctypes.c_int32()
+        check(L.rtp_cornell_point_field(self.variant, ctypes.byref(fp), ctypes.byref(nf), ctypes.byref(qc),
+                                        ctypes.byref(nq)))
+        cells = npz(qc, nq.value, np.int32)
+        self.ds = DataSet(CellSet(quads, spheres, cells), self.coord)
+        self.ds.AddField(Field("point_var", npz(fp, nf.value, np.float32)))  # CornellBox.cpp:411-416
         return self.ds
 
 

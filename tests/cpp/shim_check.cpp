@@ -75,6 +75,18 @@ int main(int argc, char** argv) {
   ss << in.rdbuf();
   EXPECT(ss.str().rfind("P3\n4 4 255\n127 255 0\n0 0 0\n", 0) == 0);
 
+  // -direct host helpers (no device): the colour table of main.cc and the
+  // GetScalar per quad over the point field
+  const std::vector<Vec4f> cmap = MainPalletColorTable().Sample(1024);
+  EXPECT(cmap.size() == 1024 && cmap[0][3] == 1.f);
+  EXPECT(std::fabs(cmap[0][0] - 13 / 255.f) < 1e-7f && std::fabs(cmap[1023][1] - 186 / 255.f) < 1e-7f);
+  EXPECT(cb.ds.quadCells.size() == 22 && cb.ds.quadCells[12] == 13);  // the sphere's vertex cell is 12
+  const std::vector<float> qs = rendering::QuadScalars(cb.ds.GetField("point_var"), cb.ds.quadCells);
+  EXPECT(qs[0] == 0.f && qs[21] > qs[12] && qs[21] <= 1.f);
+  EXPECT(throws<ErrorBadValue>([&] { cb.ds.GetField("nope"); }));
+  rendering::MapperQuadNormals qm;
+  EXPECT(throws<ErrorBadValue>([&] { qm.SetCanvas(&plain); }));
+
   if (failures) return 1;
   std::cout << "OK" << std::endl;
   return 0;

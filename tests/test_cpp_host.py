@@ -34,9 +34,7 @@ def test_shim_check(programs, tmp_path):
     assert r.stdout.strip() == "OK"
 
 
-def test_driver_out_of_scope_modes(programs):
-    r = subprocess.run([programs["rtp_path"], "-direct"], capture_output=True, text=True, timeout=60)
-    assert r.returncode == 2 and "out of scope" in r.stderr
+def test_driver_bad_sharding_args(programs):
     r = subprocess.run([programs["rtp_path"], "-hemisphere", "-rank", "3", "-world", "2"], capture_output=True,
                        text=True, timeout=60)
     assert r.returncode == 2
@@ -49,6 +47,10 @@ def test_driver_fails_loudly_without_device(programs, tmp_path):
     assert r.returncode == 1
     assert "no HIP device" in r.stderr
     assert not (tmp_path / "o.pnm").exists()
+    r = subprocess.run([programs["rtp_path"], "-x", "8", "-y", "8", "-direct"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "no HIP device" in r.stderr
+    assert not (tmp_path / "direct.pnm").exists()
 
 
 def _pnm_bytes(rgb: np.ndarray, nx: int, ny: int) -> bytes:

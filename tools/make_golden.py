@@ -50,6 +50,30 @@ def render_fixture(name, variant, nx, ny, spp, depth, pixels=None, seed_base=0, 
           f"L={live.sum() / (pixels.size * spp):.4f}, nan_px={int(np.isnan(rgba[:, :3]).any(1).sum())}")
 
 
+def direct_fixture(name, variant, nx, ny, camera=None, clip=(0.1, 5.0)):
+    """-direct mode (main.cc:120-251): colour, normals, albedo and depth of
+    one camera, full canvas, from the oracle's restatement."""
+    if ONLY and name not in ONLY:
+        return
+    t = time.time()
+    sc = oc.cornell_box(variant)
+    cam = oc.direct_setup(sc, nx, ny, clip=clip, **(camera or {}))
+    cmap = oc.sample_color_table()
+    out = {}
+    for key, aov in (("color", oc.AOV_COLOR), ("normals", oc.AOV_NORMALS), ("albedo", oc.AOV_ALBEDO)):
+        rgba, depth = oc.render_direct(sc, cam, aov, cmap=cmap)
+        out[key] = rgba
+    out["depth"] = depth
+    d = os.path.join(OUT, "direct")
+    os.makedirs(d, exist_ok=True)
+    cam_args = {k: np.asarray(v, dtype=np.float32) for k, v in (camera or {}).items()}
+    np.savez_compressed(os.path.join(d, name + ".npz"), variant=variant, nx=nx, ny=ny, clip=np.float32(clip),
+                        cmap=cmap, subset=np.int32([cam.sub_x0, cam.sub_y0, cam.sub_w, cam.sub_h]),
+                        **{"cam_" + k: v for k, v in cam_args.items()}, **out)
+    print(f"{name}: {nx}x{ny} direct, subset {cam.sub_x0},{cam.sub_y0} {cam.sub_w}x{cam.sub_h}: "
+          f"{time.time() - t:.1f}s, nan depth {int(np.isnan(out['depth']).sum())}")
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     L = oc.lib()
@@ -95,6 +119,15 @@ def main():
                    seed_base=(3 * 3840 * 2160) % (1 << 32))
     # C3 (BASELINE configs[2]): 1000-sphere scene, 2048x2048, 256 spp, depth 50 (assumed)
     render_fixture("c3_subset", 3, 2048, 2048, 256, 50, pixels=subset(2048 * 2048, 1024, 12))
+    # -direct mode (main.cc:120-251, 623-651): the default camera at the
+    # reference's default canvas (128x128), a non-square canvas, a hemisphere
+    # view (generate(): phi 0.4, theta 1.2566371) and a camera inside the box
+    direct_fixture("direct_128", 0, 128, 128)
+    direct_fixture("direct_200x120", 0, 200, 120)
+    direct_fixture("direct_hemi", 0, 96, 96, camera=dict(position=np.float32([0.19573918, 0.06558621, -1.2823226])))
+    direct_fixture("direct_inside", 2, 64, 80, camera=dict(position=np.float32([0.3, 0.7, 0.2]),
+                                                            look_at=np.float32([0.8, 0.2, 0.9]),
+                                                            view_up=np.float32([0.1, 1.0, 0.0]), fov_y=55.0))
 
 
 if __name__ == "__main__":
