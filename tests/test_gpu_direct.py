@@ -106,17 +106,22 @@ def test_view3d_mapper_api(rtp, oracle):
 
 
 def test_device_powf_matches_libm(rtp, device):
-    """Device glibc powf restatement vs numpy float32 power (the host libm's
-    powf) over a dense sample of [0, 1.01] plus special values."""
-    x = np.concatenate([np.arange(0, 0x3F8147AE, 97, dtype=np.uint32).view(np.float32),
-                        np.float32([0.0, -0.0, 1e-45, 1.0, np.inf, np.nan, 0.5, 0.999999])])
-    got = np.zeros_like(x)
+    """Device glibc powf restatement vs the host libm's powf (called through
+    ctypes: numpy's float32 power is its own SIMD code, not libm) over a
+    sample of [0, 1.01], the values just below 1, and special values."""
     import ctypes
 
-    rtp.load().rtp_eval_powf(device.handle, x.ctypes.data_as(rtp._lib.f32p), ctypes.c_float(20.0),
-                             got.ctypes.data_as(rtp._lib.f32p), x.size)
-    with np.errstate(all="ignore"):
-        want = np.power(x, np.float32(20.0))
+    libm = ctypes.CDLL("libm.so.6")
+    libm.powf.restype = ctypes.c_float
+    libm.powf.argtypes = [ctypes.c_float, ctypes.c_float]
+    x = np.concatenate([np.arange(0, 0x3F8147AE, 4099, dtype=np.uint32).view(np.float32),
+                        np.arange(0x3F7F0000, 0x3F800400, 1, dtype=np.uint32).view(np.float32),
+                        np.float32([0.0, -0.0, 1e-45, 1.0, np.inf, np.nan, 0.5, 0.999999])])
+    got = np.zeros_like(x)
+    check = rtp.load().rtp_eval_powf(device.handle, x.ctypes.data_as(rtp._lib.f32p), ctypes.c_float(20.0),
+                                     got.ctypes.data_as(rtp._lib.f32p), x.size)
+    assert check == 0
+    want = np.array([libm.powf(float(v), 20.0) for v in x], dtype=np.float32)
     assert same_bits_or_both_nan(got, want).all()
 
 
