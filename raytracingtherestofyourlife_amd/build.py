@@ -16,7 +16,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "librtp.so")
-SOURCES = ["rtp_kernels.hip", "rtp_direct.hip", "rtp_host.cpp", "rtp_direct_host.cpp", "scene_cornell.cpp"]
+SOURCES = ["rtp_kernels.hip", "rtp_direct.hip", "rtp_bvh_gpu.hip", "rtp_host.cpp", "rtp_direct_host.cpp", "scene_cornell.cpp"]
 HEADERS = ["rtp_device.hpp", "rtp_layout.hpp", "rtp_context.hpp", "glibc_powf.hpp", os.path.join("..", "..", "include", "rtp.h")]
 ARCH = os.environ.get("RTP_OFFLOAD_ARCH", "gfx950")
 

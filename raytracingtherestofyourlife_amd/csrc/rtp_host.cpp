@@ -27,6 +27,8 @@ extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::K
 extern "C" hipError_t rtp_launch_eval_primitive(int kind, const void* in, void* out, int64_t n, const uint32_t* tab,
                                                 uint32_t t1, uint32_t t2, hipStream_t stream);
 extern "C" hipError_t rtp_launch_build_ff_table(uint32_t* T, int steps, uint32_t t1, uint32_t t2, hipStream_t stream);
+extern "C" hipError_t rtp_build_bvh_gpu(const float4* d_cr, int n, float3 lo, float3 ext, rtp::BvhNode* d_nodes,
+                                        rtp::DevSphereG* d_geom, hipStream_t stream);
 extern "C" hipError_t rtp_launch_verify_fast_math(int kind, uint32_t lo, uint64_t count, unsigned long long* bad,
                                                   uint32_t* first_bad, hipStream_t stream);
 
@@ -484,10 +486,20 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     st(S.alb, ld(s->tex_rgb + 3 * s->tex_type[s->sphere_tex[k]]));
   }
   const bool use_bvh = s->n_spheres >= rtp::kBvhMinSpheres;
+  // which builder makes the sphere BVH: the host's binned SAH (better trees,
+  // O(n log n) on one core) or the device LBVH (rtp_bvh_gpu.hip) for large
+  // scenes; RTP_BVH_BUILD=host|gpu overrides
+  bool gpu_build = use_bvh && s->n_spheres >= rtp::kBvhGpuMinSpheres;
+  if (const char* bb = getenv("RTP_BVH_BUILD")) {
+    if (!std::strcmp(bb, "gpu")) gpu_build = use_bvh;
+    if (!std::strcmp(bb, "host")) gpu_build = false;
+  }
   std::vector<rtp::BvhNode> nodes;
   std::vector<rtp::DevSphereG> geom;
   if (!use_bvh) {
     for (int k = 0; k < s->n_spheres; k++) h->spheres[k] = sph[k];
+  } else if (gpu_build) {
+    h->n_nodes = 2 * s->n_spheres - 1;  // nodes and sphere records are built on the device below
   } else {
     std::vector<BvhPrim> P(s->n_spheres);
     for (int k = 0; k < s->n_spheres; k++) {
@@ -561,7 +573,31 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
       e = hipFree(*p);
       *p = nullptr;
     }
-  if (use_bvh && e == hipSuccess) {
+  if (use_bvh && gpu_build && e == hipSuccess) {
+    const int n = s->n_spheres;
+    std::vector<float4> cr(n);
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int k = 0; k < n; k++) {
+      cr[k] = make_float4(sph[k].c[0], sph[k].c[1], sph[k].c[2], sph[k].r);
+      for (int a = 0; a < 3; a++) lo[a] = std::min(lo[a], sph[k].c[a]), hi[a] = std::max(hi[a], sph[k].c[a]);
+    }
+    float4* d_cr = nullptr;
+    e = hipMalloc(&c->d_nodes, (size_t)8 * h->n_nodes * sizeof(rtp::BvhNode));
+    if (e == hipSuccess) e = hipMalloc(&c->d_sph_geom, (size_t)n * sizeof(rtp::DevSphereG));
+    if (e == hipSuccess) e = hipMalloc(&c->d_sph_all, sph.size() * sizeof(rtp::DevSphere));
+    if (e == hipSuccess) e = hipMalloc(&d_cr, (size_t)n * sizeof(float4));
+    if (e == hipSuccess) e = hipMemcpy(d_cr, cr.data(), (size_t)n * sizeof(float4), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+      e = rtp_build_bvh_gpu(d_cr, n, make_float3(lo[0], lo[1], lo[2]),
+                            make_float3(hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]), c->d_nodes, c->d_sph_geom,
+                            nullptr);
+    if (d_cr) (void)hipFree(d_cr);
+    if (e == hipSuccess)
+      e = hipMemcpy(c->d_sph_all, sph.data(), sph.size() * sizeof(rtp::DevSphere), hipMemcpyHostToDevice);
+    h->nodes = c->d_nodes;
+    h->sph_geom = c->d_sph_geom;
+    h->sph_all = c->d_sph_all;
+  } else if (use_bvh && e == hipSuccess) {
     e = hipMalloc(&c->d_nodes, nodes.size() * sizeof(rtp::BvhNode));
     if (e == hipSuccess) e = hipMalloc(&c->d_sph_geom, geom.size() * sizeof(rtp::DevSphereG));
     if (e == hipSuccess) e = hipMalloc(&c->d_sph_all, sph.size() * sizeof(rtp::DevSphere));

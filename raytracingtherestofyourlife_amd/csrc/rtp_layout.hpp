@@ -16,6 +16,7 @@ constexpr int kMaxSpp = 8388607;    // 256 slots * spp fits the pool's 32-bit sa
 constexpr int kMaxSpheres = 256;          // held inline in DevScene (scalar loads)
 constexpr int kMaxSpheresBvh = 1 << 22;   // spheres behind the BVH (global memory)
 constexpr int kBvhMinSpheres = 9;         // scenes with more spheres use the BVH
+constexpr int kBvhGpuMinSpheres = 262144;  // from this size the BVH is built on the device (rtp_bvh_gpu.hip)
 #ifndef RTP_BVH_LEAF
 #define RTP_BVH_LEAF 1  // measured best on C3: 1 < 2 < 4 < 7 (367 / 407 / 469 / 564 ms at 16 spp)
 #endif
