@@ -467,13 +467,19 @@ RTP_DEV float quad_pdf_value(const DevLights& L, f3 o, f3 v, float rmag_v) {  //
   }
   return 0;
 }
-// SpherePDFWorklet::pdf_value (PdfWorklet.h:333-346)
-RTP_DEV float sphere_pdf_value(const DevLights& L, f3 o, f3 v) {
+// SpherePDFWorklet::pdf_value (PdfWorklet.h:333-346).  ctm >= 0: the
+// caller already holds cos_theta_max = sqrt(1 - R^2/|c-o|^2) bit for bit (the
+// light-sphere generator computes the same expression from the same hit
+// point), so only lanes without it recompute.
+RTP_DEV float sphere_pdf_value(const DevLights& L, f3 o, f3 v, float ctm = -1.0f) {
   float t;
   f3 c = ld3(L.sc);
   if (sphere_hit(o, v, 0.001f, 3.40282347e+38f, c, L.srr, t)) {
-    f3 co = sub(c, o);
-    float cos_theta_max = sqrt_exact(1 - L.srr / dot(co, co));
+    float cos_theta_max = ctm;
+    if (!(ctm >= 0.0f)) {
+      f3 co = sub(c, o);
+      cos_theta_max = sqrt_exact(1 - L.srr / dot(co, co));
+    }
     float solid_angle = (float)(2 * kPi * (1 - cos_theta_max));
     return rcp_exact(solid_angle);  // 1 / solid_angle
   }

@@ -51,6 +51,9 @@
 #ifndef RTP_DEFER_RADIANCE
 #define RTP_DEFER_RADIANCE 1  // pool kernel: radiance product in the fast-forward batch
 #endif
+#ifndef RTP_REUSE_CTM
+#define RTP_REUSE_CTM 1  // sphere pdf reuses the light-sphere generator's cos_theta_max
+#endif
 #ifndef RTP_MERGED_GEN
 #define RTP_MERGED_GEN 1  // branch-free generator pass (bounce); 0: the three divergent branches
 #endif
@@ -397,6 +400,7 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
     ps.dir = sd;
   } else {  // LambertianWorklet
     f3 gen;
+    float sph_ctm = -1.0f;  // sqrt(1 - R^2/|c-hp|^2) when the generator made it (sphere_pdf_value reuses it)
     uint32_t tw = wang(seed);  // which (PdfWorklet.h:20)
     seed = tw;
 #if RTP_MERGED_GEN
@@ -425,6 +429,9 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
     // x = cos(phi)*sqrt(1-z*z) (and (c*1)*s == c*s exactly)
     const float dist2 = dot(direction, direction);
     const float q = sqrt_exact(is_cos ? 1 - r2 : 1 - L.srr / dist2);
+#if RTP_REUSE_CTM
+    sph_ctm = is_cos ? -1.0f : q;
+#endif
     const float z = is_cos ? q : 1 + r2 * (q - 1);
     const float rad = sqrt_exact(is_cos ? r2 : 1 - z * z);
     const float m = is_cos ? 2.0f : 1.0f;
@@ -473,7 +480,7 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
     const float rg = rmag(gen);
     sum += weight * quad_pdf_value(L, hp, gen, rg);
     (void)randf(seed);
-    sum += weight * sphere_pdf_value(L, hp, gen);
+    sum += weight * sphere_pdf_value(L, hp, gen, sph_ctm);
 #if RTP_DUP == 2 || RTP_DUP == 3
     {
       f3 h2 = hp;
