@@ -634,7 +634,10 @@ RTP_DEV void wave_sync() {  // order LDS traffic between lanes of this wave (no 
 #ifndef RTP_PRIO_THR
 #define RTP_PRIO_THR 0.0002f
 #endif
-constexpr int kPrioPeriod = 128;
+#ifndef RTP_PRIO_PERIOD
+#define RTP_PRIO_PERIOD 128
+#endif
+constexpr int kPrioPeriod = RTP_PRIO_PERIOD;
 
 RTP_DEV void set_priority(float lag) {  // s_setprio needs an immediate
   if (lag > RTP_PRIO_THR) __builtin_amdgcn_s_setprio(3);
