@@ -30,19 +30,21 @@ TILE = 16
 
 def tile_pixels(nx: int, ny: int, rank: int, world: int, tile: int = TILE) -> np.ndarray:
     """Pixel ids (int64, j*nx + i) of the tiles owned by `rank`; each tile in
-    row-major order, so a 64-lane wave covers a 16x4 block."""
-    if nx % tile or ny % tile:
-        raise ValueError(f"canvas {nx}x{ny} is not a multiple of the {tile}-pixel tile")
+    row-major order, so a 64-lane wave covers a 16x4 block.  Tiles on the
+    right and top edges are clipped to the canvas (1080 rows = 67.5 tiles)."""
+    if nx <= 0 or ny <= 0:
+        raise ValueError("empty canvas")
     if not 0 <= rank < world:
         raise ValueError("rank out of range")
-    tx, ty = nx // tile, ny // tile
+    tx, ty = -(-nx // tile), -(-ny // tile)
     tiles = np.arange(tx * ty)
     mine = tiles[tiles % world == rank]
     oy, ox = np.divmod(mine, tx)
     ly, lx = np.divmod(np.arange(tile * tile), tile)
     rows = (oy[:, None] * tile + ly[None, :]).astype(np.int64)
     cols = (ox[:, None] * tile + lx[None, :]).astype(np.int64)
-    return (rows * nx + cols).reshape(-1)
+    keep = (rows < ny) & (cols < nx)
+    return (rows * nx + cols)[keep]
 
 
 @dataclass(frozen=True)

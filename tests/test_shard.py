@@ -75,8 +75,15 @@ def test_tile_plan_covers_every_pixel_once():
         assert ids.size == 800 * 1600 and np.array_equal(np.sort(ids), np.arange(800 * 1600))
         sizes = [shard.tile_pixels(800, 1600, r, world).size for r in range(world)]
         assert max(sizes) - min(sizes) <= 256  # at most one tile apart
+    # canvases that are not a multiple of the tile (C4: 1080 rows = 67.5 tiles): edge tiles are clipped
+    for nx, ny, world in ((1920, 1080, 8), (100, 64, 2), (17, 33, 3)):
+        parts = [shard.tile_pixels(nx, ny, r, world) for r in range(world)]
+        ids = np.concatenate(parts)
+        assert np.array_equal(np.sort(ids), np.arange(nx * ny))
     with pytest.raises(ValueError):
-        shard.tile_pixels(100, 64, 0, 2)
+        shard.tile_pixels(0, 64, 0, 2)
+    with pytest.raises(ValueError):
+        shard.tile_pixels(64, 64, 2, 2)
 
 
 def test_sample_batches_partition():
