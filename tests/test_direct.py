@@ -146,3 +146,19 @@ def test_glibc_powf_tables_match_libm():
 
     hdr = open(os.path.join(ROOT, "raytracingtherestofyourlife_amd", "csrc", "glibc_powf.hpp")).read()
     assert E.emit(E.tables()) in hdr
+
+
+def test_find_subset_cases(oracle):
+    """FindSubset (Camera.cxx:963-1060): behind the camera -> a 1x1 subset at
+    the origin; camera inside the bounds -> the whole canvas; the default view
+    -> a rectangle strictly inside the canvas."""
+    sc = oracle.cornell_box(0)
+    c = oracle.direct_setup(sc, 33, 21, position=np.float32([0.5, 0.5, -3.0]), look_at=np.float32([0.5, 0.5, -4.0]))
+    assert [c.sub_x0, c.sub_y0, c.sub_w, c.sub_h] == [0, 0, 1, 1]
+    c = oracle.direct_setup(sc, 40, 30, position=np.float32([0.5, 0.5, 0.5]), look_at=np.float32([0.2, 0.9, 0.7]))
+    assert [c.sub_x0, c.sub_y0, c.sub_w, c.sub_h] == [0, 0, 40, 30]
+    c = oracle.direct_setup(sc, 128, 128)
+    assert 0 < c.sub_x0 and c.sub_x0 + c.sub_w < 128 and 0 < c.sub_y0 and c.sub_y0 + c.sub_h < 128
+    rgba, depth = oracle.render_direct(sc, oracle.direct_setup(sc, 33, 21, position=np.float32([0.5, 0.5, -3.0]),
+                                                               look_at=np.float32([0.5, 0.5, -4.0])), 2)
+    assert np.isnan(depth[0]) and np.all(depth[1:] == np.float32(1.001))  # the one ray misses

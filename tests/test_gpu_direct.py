@@ -141,3 +141,34 @@ def test_cpp_direct_cli_writes_reference_pnms(rtp, oracle, tmp_path):
     p = tmp_path / "want_depth.pnm"
     rtp.save_depth_pnm(str(p), wdepth, 48, 40)
     assert (tmp_path / "depth.pnm").read_text() == p.read_text()
+
+
+@pytest.mark.parametrize("nx,ny,pos,look", [
+    (1, 1, None, None),                                      # one pixel
+    (7, 40, None, None),                                     # tall canvas: FovX from SetFieldOfView
+    (33, 21, (0.5, 0.5, -3.0), (0.5, 0.5, -4.0)),            # looking away: FindSubset -> 1x1 at (0, 0)
+    (40, 30, (0.5, 0.5, 0.5), (0.2, 0.9, 0.7)),             # camera inside the bounds: full canvas
+])
+def test_direct_edge_cameras(rtp, device, oracle, nx, ny, pos, look):
+    cb = rtp.CornellBox()
+    cb.buildDataSet()
+    device.set_cornell_box(0)
+    qs = rtp.direct.quad_scalars(cb.ds.GetField("point_var").values, cb.ds.GetCellSet().quad_cells)
+    cmap = oracle.sample_color_table()
+    cam = rtp.default_camera()
+    kw = {}
+    if pos is not None:
+        cam.SetPosition(pos)
+        cam.SetLookAt(look)
+        kw = dict(position=np.float32(pos), look_at=np.float32(look))
+    sc = oracle.cornell_box(0)
+    ocam = oracle.direct_setup(sc, nx, ny, **kw)
+    if pos is not None and pos[2] == -3.0:
+        assert [ocam.sub_x0, ocam.sub_y0, ocam.sub_w, ocam.sub_h] == [0, 0, 1, 1]
+    if pos is not None and pos[2] == 0.5:
+        assert [ocam.sub_x0, ocam.sub_y0, ocam.sub_w, ocam.sub_h] == [0, 0, nx, ny]
+    got = rtp.direct.render_direct(device, cam, nx, ny, qs, cmap, aovs=7, depth=True)
+    for key, aov in (("color", 1), ("normals", 2), ("albedo", 4)):
+        want, wdepth = oracle.render_direct(sc, ocam, aov, cmap=cmap)
+        _assert_same(got[key], want, f"{nx}x{ny} {key}")
+        _assert_same(got["depth"], wdepth, f"{nx}x{ny} depth")
