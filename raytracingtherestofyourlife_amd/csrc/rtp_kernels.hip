@@ -54,6 +54,9 @@
 #ifndef RTP_REUSE_CTM
 #define RTP_REUSE_CTM 1  // sphere pdf reuses the light-sphere generator's cos_theta_max
 #endif
+#ifndef RTP_CRIT_FF
+#define RTP_CRIT_FF 100  // pool kernel: lag (per mille of the wave's average samples) that makes a pixel critical
+#endif
 #ifndef RTP_MERGED_GEN
 #define RTP_MERGED_GEN 1  // branch-free generator pass (bounce); 0: the three divergent branches
 #endif
@@ -737,6 +740,7 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
   }
 
   int published = 0;  // wave-uniform: finished samples already added to p.progress
+  bool critical_ff = false;  // wave-uniform: a critical (far-lagging) pixel waits in the FF queue
 
   bool has_path = false;
   int slot = 0;
@@ -752,7 +756,8 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
     const int n_idle = __popcll(idle);
     const int n_ready = ready_tail - ready_head;
     const int n_ff = ff_tail - ff_head;
-    if (n_ready < n_idle && n_ff > 0) {
+    if ((n_ready < n_idle || critical_ff) && n_ff > 0) {
+      critical_ff = false;
       // ---- batch RNG fast-forward over the remaining dead depths of finished
       //      samples (1 + {2,3,2} draws per depth) ----
       const unsigned long long t0 = want_dbg ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -925,6 +930,15 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
     }
     const uint64_t fin = __ballot(ended);
     if (ended) q_ff[(ff_tail + (int)lane_rank(fin)) & (kPool - 1)] = (uint16_t)slot;
+#if RTP_CRIT_FF > 0
+    // A pixel whose finished samples lag the wave's average by more than
+    // RTP_CRIT_FF/1000 runs its sample chain on the critical path (its path
+    // length keeps it behind): its fast-forward is not left waiting for the
+    // READY queue to run dry -- the batch runs in the next iteration.
+    if (__ballot(ended && (uint64_t)s_samples[slot] * (uint64_t)n_slots * 1000u <
+                              (uint64_t)ff_tail * (uint64_t)(1000 - RTP_CRIT_FF)))
+      critical_ff = true;
+#endif
     ff_tail += __popcll(fin);
     wave_sync();
     if (RTP_PRIO_BALANCE && ff_tail - published >= kPrioPeriod) {
