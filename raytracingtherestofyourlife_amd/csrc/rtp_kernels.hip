@@ -54,6 +54,9 @@
 #ifndef RTP_REUSE_CTM
 #define RTP_REUSE_CTM 1  // sphere pdf reuses the light-sphere generator's cos_theta_max
 #endif
+#ifndef RTP_FF_MARGIN
+#define RTP_FF_MARGIN 12  // pool kernel: fast-forward when READY holds fewer than idle lanes + this
+#endif
 #ifndef RTP_CRIT_FF
 #define RTP_CRIT_FF 100  // pool kernel: lag (per mille of the wave's average samples) that makes a pixel critical
 #endif
@@ -756,7 +759,7 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
     const int n_idle = __popcll(idle);
     const int n_ready = ready_tail - ready_head;
     const int n_ff = ff_tail - ff_head;
-    if ((n_ready < n_idle || critical_ff) && n_ff > 0) {
+    if ((n_ready < n_idle + RTP_FF_MARGIN || critical_ff) && n_ff > 0) {
       critical_ff = false;
       // ---- batch RNG fast-forward over the remaining dead depths of finished
       //      samples (1 + {2,3,2} draws per depth) ----
