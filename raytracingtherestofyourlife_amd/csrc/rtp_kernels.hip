@@ -57,6 +57,9 @@
 #ifndef RTP_FF_MARGIN
 #define RTP_FF_MARGIN 12  // pool kernel: fast-forward when READY holds fewer than idle lanes + this
 #endif
+#ifndef RTP_URGENT_PERMILLE
+#define RTP_URGENT_PERMILLE 0  // pool kernel: READY front for pixels at most this far above the average samples
+#endif
 #ifndef RTP_CRIT_FF
 #define RTP_CRIT_FF 100  // pool kernel: lag (per mille of the wave's average samples) that makes a pixel critical
 #endif
@@ -840,7 +843,8 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
       // paths, back sooner) take more than their share of lanes, so the
       // expensive pixels' sequential sample chains ran on alone at the end
       // (17% of bounce steps with ~12 of 64 lanes live).
-      const bool urgent = again && (uint64_t)s_samples[fslot] * (uint64_t)n_slots <= (uint64_t)ff_tail;
+      const bool urgent = again && (uint64_t)s_samples[fslot] * (uint64_t)n_slots * 1000u <=
+                                       (uint64_t)ff_tail * (uint64_t)(1000 + RTP_URGENT_PERMILLE);
       const uint64_t pu = __ballot(urgent), pn = __ballot(again && !urgent);
       ready_head -= __popcll(pu);
       if (urgent) q_ready[(ready_head + (int)lane_rank(pu)) & (kPool - 1)] = (uint16_t)fslot;
