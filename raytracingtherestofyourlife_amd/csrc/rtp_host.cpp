@@ -119,9 +119,11 @@ bool bit_equal(const float* a, const float* b, int n) { return std::memcmp(a, b,
 // k = 32 >> j over all 2^32 states (16 GiB each; built once per device and
 // process, shared by every context).  The pool kernel's fast-forward then
 // takes a few table reads instead of ~150 hashes per sample.  RTP_FF_TABLES=n
-// (0..4, default 3: 48 GiB) sets how many tables (32, 16, 8, 4 depths) to build;
+// (0..4, default 4: 64 GiB) sets how many tables (32, 16, 8, 4 depths) to build;
 // fewer are built when the device lacks the memory (8 GiB kept free).  On C2,
-// 2 / 3 / 4 tables measured 170.8 / 168.9 / 169.8 ms per render.
+// 2 / 3 / 4 tables measured 170.8 / 168.9 / 169.8 ms per render before the
+// critical-pixel fast-forward trigger, and 3 / 4 tables 148.2 / 147.0 ms after
+// it (3 interleaved rounds, same box).
 struct FfTables {
   uint32_t* t[rtp::kFfTables] = {};
   bool tried = false;
@@ -135,7 +137,7 @@ const FfTables& ff_tables(int device) {
   FfTables& T = g_ff[device & 63];
   if (T.tried) return T;
   T.tried = true;
-  int want = 3;
+  int want = 4;
   if (const char* env = getenv("RTP_FF_TABLES")) want = std::max(0, std::min(rtp::kFfTables, atoi(env)));
   const size_t bytes = (size_t)4 << 32;
   const uint32_t t1 = which_threshold(2), t2 = which_threshold(3);
