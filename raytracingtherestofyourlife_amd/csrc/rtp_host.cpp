@@ -119,11 +119,12 @@ bool bit_equal(const float* a, const float* b, int n) { return std::memcmp(a, b,
 // k = 32 >> j over all 2^32 states (16 GiB each; built once per device and
 // process, shared by every context).  The pool kernel's fast-forward then
 // takes a few table reads instead of ~150 hashes per sample.  RTP_FF_TABLES=n
-// (0..4, default 4: 64 GiB) sets how many tables (32, 16, 8, 4 depths) to build;
+// (0..6, default 4: 64 GiB) sets how many tables (32, 16, 8, 4, 2, 1 depths) to build;
 // fewer are built when the device lacks the memory (8 GiB kept free).  On C2,
 // 2 / 3 / 4 tables measured 170.8 / 168.9 / 169.8 ms per render before the
 // critical-pixel fast-forward trigger, and 3 / 4 tables 148.2 / 147.0 ms after
-// it (3 interleaved rounds, same box).
+// it; 4 / 5 / 6 tables (down to single dead steps, no hashing left) 146.7 /
+// 147.9 / 149.3 ms (3 interleaved rounds each, same box).
 struct FfTables {
   uint32_t* t[rtp::kFfTables] = {};
   bool tried = false;

@@ -124,7 +124,7 @@ struct DevCamera {
   float eye[3], nlook[3], dx[3], dy[3];
 };
 
-constexpr int kFfTables = 4;  // jump tables for 32, 16, 8, 4 dead depths
+constexpr int kFfTables = 6;  // jump tables for 32, 16, 8, 4, 2, 1 dead depths
 
 struct KParams {
   DevCamera cam;
