@@ -225,6 +225,12 @@ rtp_status rtp_eval_primitive(rtp_context* ctx, int32_t kind, const void* in, vo
  * per-wave records (waves * kDbgCounters values) instead. */
 int32_t rtp_debug_counters(rtp_context* ctx, uint64_t* out, int32_t n_out);
 
+/* Diagnostics: the closest hit of n rays (o, d: 6 floats each, host memory)
+ * through the quad prefilter and through the exact scan of every quad.
+ * out (host, 7 u32 per ray): prefiltered (t bits, kind, index), exact (t
+ * bits, kind, index), 1 if the ray fell back to the exact scan. */
+rtp_status rtp_debug_closest_hit(rtp_context* ctx, const float* rays, int64_t n, uint32_t* out);
+
 /* Diagnostics: exhaustively compare a fast device arithmetic sequence with the
  * IEEE operation for every float bit pattern in [lo_bits, hi_bits].  kind 0:
  * rcp (v_rcp + 1 Newton step) vs 1.0f/x; 1: rcp + remainder correction; 2:

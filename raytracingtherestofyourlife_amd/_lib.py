@@ -63,7 +63,7 @@ RTP_AOV_COLOR, RTP_AOV_NORMALS, RTP_AOV_ALBEDO = 1, 2, 4
 EXPORTED_SYMBOLS = [
     "rtp_last_error", "rtp_abi_version", "rtp_create", "rtp_destroy", "rtp_set_scene", "rtp_render",
     "rtp_render_device", "rtp_render_pixels", "rtp_normalize", "rtp_write_pnm", "rtp_cornell_box",
-    "rtp_eval_primitive", "rtp_debug_counters", "rtp_verify_fast_math",
+    "rtp_eval_primitive", "rtp_debug_counters", "rtp_verify_fast_math", "rtp_debug_closest_hit",
     "rtp_render_direct", "rtp_render_direct_device", "rtp_sample_color_table", "rtp_quad_scalars",
     "rtp_cornell_point_field", "rtp_write_pnm_depth", "rtp_eval_powf",
 ]
@@ -117,6 +117,7 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.rtp_write_pnm.argtypes = [ctypes.c_char_p, f32p, ctypes.c_int32, ctypes.c_int32]
     L.rtp_cornell_box.argtypes = [ctypes.c_int32, ctypes.POINTER(RtpSceneDesc)]
     L.rtp_eval_primitive.argtypes = [vp, ctypes.c_int32, vp, vp, ctypes.c_int64]
+    L.rtp_debug_closest_hit.argtypes = [vp, vp, ctypes.c_int64, vp]
     L.rtp_debug_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32]
     L.rtp_verify_fast_math.argtypes = [vp, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32,
                                        ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]

@@ -29,6 +29,8 @@ extern "C" hipError_t rtp_launch_eval_primitive(int kind, const void* in, void* 
 extern "C" hipError_t rtp_launch_build_ff_table(uint32_t* T, int steps, uint32_t t1, uint32_t t2, hipStream_t stream);
 extern "C" hipError_t rtp_build_bvh_gpu(const float4* d_cr, int n, float3 lo, float3 ext, rtp::BvhNode* d_nodes,
                                         rtp::DevSphereG* d_geom, hipStream_t stream);
+extern "C" hipError_t rtp_launch_eval_closest(const rtp::DevScene* scene, const float* rays, uint32_t* out,
+                                              int64_t n, int bvh, hipStream_t stream);
 extern "C" hipError_t rtp_launch_verify_fast_math(int kind, uint32_t lo, uint64_t count, unsigned long long* bad,
                                                   uint32_t* first_bad, hipStream_t stream);
 
@@ -111,6 +113,70 @@ void fill_quad(rtp::DevQuad& Q, v3 q, v3 r, v3 s, v3 t) {
 }
 
 bool bit_equal(const float* a, const float* b, int n) { return std::memcmp(a, b, sizeof(float) * n) == 0; }
+
+// Closest-hit prefilter tables (rtp_kernels.hip closest_hit):
+// the quads of groups 0..5 (kinds 1..6, edges along two axes) lie in a plane
+// x[axis] = const, bit for bit.  Each gets that plane and a box around its
+// vertices in the other two coordinates, widened outward by a few ulps so
+// that the float box contains the real one.  Enabled only when every such
+// quad qualifies, they fit kMaxPre, and the scene is within the coordinate
+// range the kernel's error margins assume (|x| <= kPreLim).
+constexpr float kPreLim = 16.0f;
+void setup_prefilter(rtp::DevScene* h, const rtp_scene_desc* s, const std::vector<int>& kept) {
+  h->n_pre = 0;
+  for (int a = 0; a <= 3; a++) h->pre_begin[a] = 0;
+  h->pre_scale = 0.0f;
+  const int n = h->kind_begin[6];
+  if (n <= 0 || n > rtp::kMaxPre) return;
+  const char* e = getenv("RTP_PREFILTER");
+  if (e && e[0] == '0') return;
+  std::vector<int> axis_of(n);
+  std::vector<rtp::PreQuad> pq(n);
+  float scale = 0.0f;
+  for (int q = 0; q < n; q++) {
+    const rtp::DevQuad& Q = h->quads[q];
+    const rtp::QuadKindMasks& K = rtp::kQuadKind[Q.kind];
+    const int flat = 7 & ~(K.m01 | K.m03);
+    if (Q.kind < 1 || Q.kind > 6 || (flat != 1 && flat != 2 && flat != 4)) return;
+    const int a = flat == 1 ? 0 : flat == 2 ? 1 : 2, b = (a + 1) % 3, c = (a + 2) % 3;
+    const int32_t* id = s->quad_points + 4 * kept[Q.orig];
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    const float x = s->points[3 * id[0] + a];
+    for (int k = 0; k < 4; k++) {
+      const float* v = s->points + 3 * id[k];
+      if (!(v[a] == x)) return;  // not in one axis plane
+      for (int j = 0; j < 3; j++) {
+        if (!std::isfinite(v[j])) return;
+        lo[j] = std::min(lo[j], (double)v[j]);
+        hi[j] = std::max(hi[j], (double)v[j]);
+        scale = std::max(scale, std::fabs(v[j]));
+      }
+    }
+    auto centre_half = [&](int j, float& cen, float& half) {
+      cen = (float)(0.5 * (lo[j] + hi[j]));
+      const double need = std::max(hi[j] - (double)cen, (double)cen - lo[j]);
+      half = (float)need;
+      for (int u = 0; u < 2; u++) half = std::nextafter(half, INFINITY);  // >= need after rounding
+    };
+    rtp::PreQuad& P = pq[q];
+    std::memset(&P, 0, sizeof(P));
+    P.x = x;
+    centre_half(b, P.cb, P.rb);
+    centre_half(c, P.cc, P.rc);
+    P.qpos = q;
+    axis_of[q] = a;
+  }
+  if (!(scale <= kPreLim)) return;
+  int pos = 0;
+  for (int a = 0; a < 3; a++) {
+    h->pre_begin[a] = pos;
+    for (int q = 0; q < n; q++)
+      if (axis_of[q] == a) h->pre[pos++] = pq[q];
+  }
+  h->pre_begin[3] = pos;
+  h->pre_scale = scale;
+  h->n_pre = n;
+}
 
 // RNG jump tables.  A dead depth consumes 1 + {2,3,2} draws chosen by the
 // `which` draw against two constant thresholds (lightables = 2,
@@ -449,6 +515,7 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     }
     h->kind_begin[rtp::kQuadKinds] = pos;
   }
+  setup_prefilter(h, s, kept);
   h->n_quads = (int32_t)kept.size();
   // the -direct mode's inputs: kept quad -> reference index, and the shape
   // bounds (union of the quads' padded AABBs, AABBSurface.h:36-78)
@@ -883,6 +950,27 @@ rtp_status rtp_eval_primitive(rtp_context* c, int32_t kind, const void* in, void
   (void)hipFree(din);
   if (dout) (void)hipFree(dout);
   if (e != hipSuccess) return hip_fail(e, "rtp_eval_primitive");
+  return RTP_OK;
+}
+
+// Diagnostics: the closest hit of host rays with and without the quad
+// prefilter (rtp_eval_closest_kernel; 7 u32 per ray).
+rtp_status rtp_debug_closest_hit(rtp_context* c, const float* rays, int64_t n, uint32_t* out) {
+  if (!c || !rays || !out || n < 0) return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_debug_closest_hit: bad arguments");
+  if (!c->d_scene) return fail(RTP_ERR_NO_SCENE, "rtp_debug_closest_hit: no scene set");
+  if (n == 0) return RTP_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  void *din = nullptr, *dout = nullptr;
+  HIP_TRY(hipMalloc(&din, (size_t)n * 24));
+  hipError_t e = hipMalloc(&dout, (size_t)n * 28);
+  if (e == hipSuccess) e = hipMemcpy(din, rays, (size_t)n * 24, hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = rtp_launch_eval_closest(c->d_scene, static_cast<const float*>(din), static_cast<uint32_t*>(dout), n,
+                                c->use_bvh ? 1 : 0, nullptr);
+  if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)n * 28, hipMemcpyDeviceToHost);
+  (void)hipFree(din);
+  if (dout) (void)hipFree(dout);
+  if (e != hipSuccess) return hip_fail(e, "rtp_debug_closest_hit");
   return RTP_OK;
 }
 

@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "rtp_device.hpp"
@@ -225,8 +226,105 @@ RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
   }
 }
 
+// qshade: the block's LDS copy of the quads' shading data (n, alb, mt) so
+// the hit's material is an LDS gather instead of a global one.
+// Each record: n, alb, mt, pad (8 words); with RTP_PRE_LDS the QuadTest copy
+// (24 words) for the prefilter's per-lane exact test follows.
+#ifndef RTP_PRE_LDS
+#define RTP_PRE_LDS 0
+#endif
+constexpr int kLdsQuads = 64, kQTestOffset = 8, kQShadeFloats = RTP_PRE_LDS ? 32 : 8;
+static_assert(!RTP_PRE_LDS || kQTestOffset + sizeof(QuadTest) / 4 == kQShadeFloats, "qshade record layout");
+
+// The block's LDS copy of the quads' shading data and QuadTest records.
+RTP_DEV void fill_qshade(const DevScene* __restrict__ sc, float* s_qshade) {
+  for (int i = threadIdx.x; i < sc->n_quads * kQShadeFloats; i += blockDim.x) {
+    const DevQuad& Q = sc->quads[i / kQShadeFloats];
+    const int f = i % kQShadeFloats, g = f - kQTestOffset;
+    const float* qw = reinterpret_cast<const float*>(&Q);
+    s_qshade[i] = f < 3                                        ? Q.n[f]
+                  : f < 6                                      ? Q.alb[f - 3]
+                  : f == 6                                     ? __int_as_float(Q.mt)
+                  : f < kQTestOffset                           ? 0.f
+                  : g < (int)(offsetof(QuadTest, para) / 4)    ? qw[g]
+                  : g == (int)(offsetof(QuadTest, para) / 4)   ? __int_as_float(Q.para)
+                  : g == (int)(offsetof(QuadTest, key_lo) / 4) ? __uint_as_float(Q.key_lo)
+                                                               : 0.f;
+  }
+}
+
+// Closest-hit prefilter over the axis-plane quads (kinds 1..6).
+// The exact Lagae-Dutre test costs ~40 VALU per quad and every quad meets
+// some lane of a wave, so the scan paid it for all of them.  The prefilter
+// instead takes, per quad, the ray's parameter at the quad's plane and the
+// hit point's distance outside the quad's box, both in a few ops, with an
+// error margin m >= the difference between these approximations and the
+// exact test's own roundings:
+//   m = 2^-18 * (|t| * max(max|d|, 1) + max|o| + scene scale + 1),
+// about six times the worst case of either computation (a handful of
+// roundings each of |t*d|, |o| and the vertex coordinates).
+// A quad the exact test accepts (0.001 < t, inside) is therefore a
+// candidate, and t - m is a lower bound of its exact t.  Each lane keeps its
+// two smallest lower bounds, runs the exact test on the first (the generic
+// kind-0 arithmetic on the block's LDS copy of the quad; equal to the kind's own
+// sequence because the skipped terms are exact zeros), and is done when the
+// second lower bound exceeds the best exact hit: every other candidate's
+// exact t is larger, so it loses whatever its index.  Otherwise -- near an
+// edge, a near tie, no finite ray, coordinates beyond kPreLim -- the lane
+// runs the exact scan of every axis-plane quad, as without the prefilter.
+#ifndef RTP_PREFILTER
+#define RTP_PREFILTER 1
+#endif
+#ifndef RTP_PRE_ASM
+#define RTP_PRE_ASM 1  // v_and_or_b32 / v_med3_u32 in the prefilter loop (the compiler emits 2 + 2 ops)
+#endif
+#ifndef RTP_LDS_PAD
+#define RTP_LDS_PAD 0  // (experiments) extra bytes of pool LDS per block
+#endif
+constexpr float kPreTmin = 0.0005f;  // candidates: approximate t above this (accepted hits: t > 0.001)
+constexpr float kPreLimD = 16.0f;    // larger |o| or |d| components: exact scan (margin bound below tmin)
+constexpr float kPreK = 0x1p-18f;    // margin factor, 64 units of 2^-24
+template <int A>
+RTP_DEV float comp(f3 v) {
+  if constexpr (A == 0) return v.x;
+  else if constexpr (A == 1) return v.y;
+  else return v.z;
+}
+// k1 <= k2: the two smallest candidate keys {bits(t - m) & ~31, quad position}
+// (positive floats order like their bit patterns; rounding the low bits
+// down keeps the lower bound).  No candidate: ~0u.
+template <int A>
+RTP_DEV void pre_axis(const DevScene* __restrict__ sc, f3 o, f3 d, float ma, float mb, uint32_t& k1, uint32_t& k2) {
+  constexpr int B = (A + 1) % 3, C = (A + 2) % 3;
+  const int b = sc->pre_begin[A], e = sc->pre_begin[A + 1];
+  if (b == e) return;
+  const float inv = __builtin_amdgcn_rcpf(comp<A>(d));
+  const float oa = comp<A>(o), ob = comp<B>(o), oc = comp<C>(o), db = comp<B>(d), dc = comp<C>(d);
+  for (int i = b; i < e; i++) {
+    const PreQuad& P = sc->pre[i];
+    const float t = (P.x - oa) * inv;
+    const float ub = fabsf(__builtin_fmaf(t, db, ob) - P.cb) - P.rb;
+    const float uc = fabsf(__builtin_fmaf(t, dc, oc) - P.cc) - P.rc;
+    const float m = __builtin_fmaf(fabsf(t), ma, mb);
+    // t = +-inf (d[A] ~ 0) gives NaN or inf here and at worst a key above
+    // every finite one; the exact test rejects such a quad (|det| < eps)
+    const bool ok = (fmaxf(ub, uc) <= m) & (t > kPreTmin);
+#if RTP_PRE_ASM
+    uint32_t key;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(key) : "v"(__float_as_uint(t - m)), "v"(~31u), "s"((uint32_t)P.qpos));
+    key = ok ? key : ~0u;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(k2) : "v"(k1), "v"(k2), "v"(key));
+#else
+    const uint32_t key = ok ? ((__float_as_uint(t - m) & ~31u) | (uint32_t)P.qpos) : ~0u;
+    k2 = min(k2, max(k1, key));
+#endif
+    k1 = min(k1, key);
+  }
+}
+
 template <bool kBvh>
-RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d) {
+RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, const float* qshade = nullptr,
+                        uint32_t* full_out = nullptr) {
   Hit h{3.40282347e+38f, -1, 0};
   int best = 0x7fffffff;
   const float tmin = 0.001f;
@@ -256,20 +354,56 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d) {
 #undef RTP_SCAN2
   }
 #endif
-  // scan order of the host's grouping: kinds 1..kQuadKinds-1, then 0
+  // the (t, orig) key minimum: the order the kinds are scanned in is free
 #if RTP_HIT_KEY
   uint64_t key = kNoHitKey;
-  scan_kind<1>(sc, 0, o, d, key);
-  scan_kind<2>(sc, 1, o, d, key);
-  scan_kind<3>(sc, 2, o, d, key);
-  scan_kind<4>(sc, 3, o, d, key);
-  scan_kind<5>(sc, 4, o, d, key);
-  scan_kind<6>(sc, 5, o, d, key);
+  // kinds 7..10 and 0: the exact scan, always (their keys are final)
   scan_kind<7>(sc, 6, o, d, key);
   scan_kind<8>(sc, 7, o, d, key);
   scan_kind<9>(sc, 8, o, d, key);
   scan_kind<10>(sc, 9, o, d, key);
   scan_kind<0>(sc, 10, o, d, key);
+  bool full = true;  // this lane needs the exact scan of the axis-plane quads (kinds 1..6)
+#if RTP_PREFILTER
+  const bool pre = qshade != nullptr && sc->n_pre > 0;  // wave-uniform
+  if (pre) {
+    const bool lane_ok = (int)(fabsf(o.x) <= kPreLimD) & (int)(fabsf(o.y) <= kPreLimD) &
+                         (int)(fabsf(o.z) <= kPreLimD) & (int)(fabsf(d.x) <= kPreLimD) &
+                         (int)(fabsf(d.y) <= kPreLimD) & (int)(fabsf(d.z) <= kPreLimD);
+    const float dmax = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fmaxf(fabsf(d.z), 1.0f));
+    const float omax = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+    const float ma = kPreK * dmax, mb = kPreK * (omax + (sc->pre_scale + 1.0f));
+    uint32_t k1 = ~0u, k2 = ~0u;
+    pre_axis<0>(sc, o, d, ma, mb, k1, k2);
+    pre_axis<1>(sc, o, d, ma, mb, k1, k2);
+    pre_axis<2>(sc, o, d, ma, mb, k1, k2);
+    if (lane_ok && k1 != ~0u) {  // (finite o, d: the generic arithmetic equals the kind's)
+#if RTP_PRE_LDS
+      const QuadTest& Q = *reinterpret_cast<const QuadTest*>(qshade + (k1 & 31u) * kQShadeFloats + kQTestOffset);
+#else
+      const DevQuad& Q = sc->quads[k1 & 31u];  // a per-lane (vector) load: measured faster than the LDS copy
+#endif
+      float t;
+      const bool ok = quad_hit_masked<0>(Q, o, d, t);
+      const uint64_t kq = (uint64_t)__float_as_uint(t) << 32 | Q.key_lo;
+      key = (ok && t > 0.001f && kq < key) ? kq : key;
+    }
+    full = !lane_ok || (k2 & ~31u) <= (uint32_t)(key >> 32);  // k2 = ~0u (none) never is
+  }
+  if (full_out) *full_out = pre && full;
+#else
+  if (full_out) *full_out = 0;
+#endif
+  if (__ballot(full)) {
+    if (full) {
+      scan_kind<1>(sc, 0, o, d, key);
+      scan_kind<2>(sc, 1, o, d, key);
+      scan_kind<3>(sc, 2, o, d, key);
+      scan_kind<4>(sc, 3, o, d, key);
+      scan_kind<5>(sc, 4, o, d, key);
+      scan_kind<6>(sc, 5, o, d, key);
+    }
+  }
   (void)best;
   if (key != kNoHitKey) {
     h.t = __uint_as_float((uint32_t)(key >> 32));
@@ -337,10 +471,8 @@ RTP_DEV unsigned long long stamp(bool on) { return on ? __builtin_amdgcn_s_memti
 // kDeferDead: a path that misses or hits the light at depth k leaves its
 // depth-k draws (which + generator, exactly one dead step) to the caller's
 // fast-forward instead of drawing them here.
-// qshade (nullable): the block's LDS copy of the quads' shading data
-// (n, alb, mt; kQShadeFloats per quad) so the hit's material is an LDS
-// gather instead of a global one.
-constexpr int kLdsQuads = 64, kQShadeFloats = 8;
+// qshade (nullable): the block's LDS quad table (fill_qshade); also turns
+// on the closest-hit prefilter.
 template <bool kBvh, bool kDeferDead = false>
 RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3& emit, float4* __restrict__ hist_d,
                    int D, unsigned long long* dbg = nullptr, const float* qshade = nullptr) {
@@ -351,7 +483,7 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
   const f3 org = ps.org, dir = ps.dir;
   const int d = ps.d;
   // intersect + CollectIntersecttWorklet (SurfaceWorklets.h:104-109)
-  Hit h = closest_hit<kBvh>(sc, org, dir);
+  Hit h = closest_hit<kBvh>(sc, org, dir, qshade);
 #if RTP_DUP == 1
   {
     f3 o2 = org;
@@ -671,7 +803,7 @@ template <bool kStats, bool kBvh>
 #define RTP_POOL_VGPR_ATTR
 #endif
 __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_ATTR rtp_render_pool(const DevScene* __restrict__ sc, KParams p, int n_waves) {
-  __shared__ __align__(16) unsigned char smem[kPoolLdsBytes];
+  __shared__ __align__(16) unsigned char smem[kPoolLdsBytes + RTP_LDS_PAD];
   __shared__ float s_qshade[kLdsQuads * kQShadeFloats];
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
@@ -679,11 +811,7 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
   // the quads' shading data into LDS (the block's only barrier, before any wave leaves)
   const bool qshade_lds = RTP_QSHADE_LDS && sc->n_quads <= kLdsQuads;
   if (qshade_lds) {
-    for (int i = threadIdx.x; i < sc->n_quads * kQShadeFloats; i += blockDim.x) {
-      const DevQuad& Q = sc->quads[i / kQShadeFloats];
-      const int f = i % kQShadeFloats;
-      s_qshade[i] = f < 3 ? Q.n[f] : f < 6 ? Q.alb[f - 3] : f == 6 ? __int_as_float(Q.mt) : 0.f;
-    }
+    fill_qshade(sc, s_qshade);
   }
   __syncthreads();
   if (w >= n_waves) return;  // whole wave leaves; no block-level barriers follow
@@ -1006,6 +1134,30 @@ __global__ void rtp_eval_primitive_kernel(int kind, const void* in, void* out, i
   }
 }
 
+// closest_hit with and without the prefilter on a list of rays (o, d: 6
+// floats each): out[7 i ..] = prefiltered (t bits, kind, idx), exact scan
+// (t bits, kind, idx), 1 if the lane fell back to the exact scan.
+template <bool kBvh>
+__global__ void __launch_bounds__(256) rtp_eval_closest_kernel(const DevScene* __restrict__ sc,
+                                                               const float* __restrict__ rays, uint32_t* out,
+                                                               int64_t n) {
+  __shared__ float s_qshade[kLdsQuads * kQShadeFloats];
+  const bool lds = sc->n_quads <= kLdsQuads;
+  if (lds) fill_qshade(sc, s_qshade);
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* r = rays + 6 * i;
+  const f3 o = mk(r[0], r[1], r[2]), d = mk(r[3], r[4], r[5]);
+  uint32_t full = 0;
+  const Hit a = closest_hit<kBvh>(sc, o, d, lds ? s_qshade : nullptr, &full);
+  const Hit b = closest_hit<kBvh>(sc, o, d);
+  uint32_t* w = out + 7 * i;
+  w[0] = __float_as_uint(a.t), w[1] = (uint32_t)a.kind, w[2] = (uint32_t)a.idx;
+  w[3] = __float_as_uint(b.t), w[4] = (uint32_t)b.kind, w[5] = (uint32_t)b.idx;
+  w[6] = full;
+}
+
 // Dead-step jump table: T[s] = dead_step^steps(s) for s in [base, base+count).
 __global__ void rtp_build_ff_table_kernel(uint32_t* __restrict__ T, int steps, uint32_t t1, uint32_t t2, uint64_t base,
                                           uint64_t count) {
@@ -1073,6 +1225,16 @@ int pool_resident_waves(bool stats, bool bvh) {
   const int nb = stats ? (bvh ? resident_blocks_per_cu<true, true>() : resident_blocks_per_cu<true, false>())
                        : (bvh ? resident_blocks_per_cu<false, true>() : resident_blocks_per_cu<false, false>());
   c = cus * nb * rtp::kWavesPerBlock;
+  if (const char* v = getenv("RTP_VERBOSE")) {
+    if (v[0] == '1') {
+      int lds_cu = 0;
+      (void)hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev);
+      hipFuncAttributes fa{};
+      (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(rtp::rtp_render_pool<false, false>));
+      fprintf(stderr, "rtp: pool kernel %d CUs x %d blocks of %d waves; LDS %zu B per block, %d B per CU; %d VGPRs\n",
+              cus, nb, rtp::kWavesPerBlock, (size_t)fa.sharedSizeBytes, lds_cu, fa.numRegs);
+    }
+  }
   return c;
 }
 int kernel_variant() {
@@ -1100,6 +1262,14 @@ extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int bvh, int* variant_ou
   return RTP_DEFER_RADIANCE ? W * rtp::kPool : W * 64;
 }
 
+extern "C" hipError_t rtp_launch_eval_closest(const rtp::DevScene* scene, const float* rays, uint32_t* out,
+                                              int64_t n, int bvh, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  const dim3 g((unsigned)((n + 255) / 256)), b(256);
+  if (bvh) hipLaunchKernelGGL(rtp::rtp_eval_closest_kernel<true>, g, b, 0, stream, scene, rays, out, n);
+  else hipLaunchKernelGGL(rtp::rtp_eval_closest_kernel<false>, g, b, 0, stream, scene, rays, out, n);
+  return hipGetLastError();
+}
 extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::KParams* p, int variant, int waves,
                                         int bvh, hipStream_t stream) {
   if (p->npix <= 0) return hipSuccess;

@@ -6,6 +6,7 @@
 // normalised quad normals, light-quad area, r*r ...), so the per-ray
 // arithmetic in the kernel is bit-identical to the reference's.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 namespace rtp {
@@ -55,6 +56,18 @@ struct alignas(16) DevQuad {
   int32_t pad[3];
 };
 
+// The fields of DevQuad the Lagae-Dutre test reads, plus its hit-key word:
+// the pool kernel's LDS copy for the prefilter's per-lane exact test.
+struct alignas(16) QuadTest {
+  float vv[3][2];
+  float e01[3], e03[3];
+  float e21[3], e23[3];
+  int32_t para;
+  uint32_t key_lo;
+  int32_t pad[4];
+};
+static_assert(offsetof(DevQuad, e23) == offsetof(QuadTest, e23), "QuadTest leads like DevQuad");
+
 struct alignas(16) DevSphere {
   float c[3];
   float r;
@@ -100,6 +113,19 @@ struct alignas(16) DevLights {
   int32_t pad[2];
 };
 
+// Axis-plane quad of the closest-hit prefilter (kinds 1..6: every vertex
+// shares coordinate `axis` bit for bit).  (cb, cc) +- (rb, rc) bounds the
+// quad in the two other coordinates (b = axis+1, c = axis+2 mod 3), widened
+// outward on the host.  Read with uniform (scalar) loads.
+constexpr int kMaxPre = 32;  // prefiltered quads; the key packs the index in 5 bits
+struct alignas(16) PreQuad {
+  float x;         // the plane: coordinate `axis` of every vertex
+  float cb, rb;    // centre / half extent along axis+1
+  float cc, rc;    // centre / half extent along axis+2
+  int32_t qpos;    // position in DevScene::quads
+  int32_t pad[2];
+};
+
 struct alignas(16) DevScene {
   int32_t n_quads;
   int32_t n_spheres;
@@ -117,6 +143,14 @@ struct alignas(16) DevScene {
   DevLights light;
   DevQuad quads[kMaxQuads];
   DevSphere spheres[kMaxSpheres];
+  // closest-hit prefilter over the axis-plane quads (groups 0..5 = kinds 1..6):
+  // n_pre == kind_begin[6] when enabled, else 0; pre[] grouped by plane axis,
+  // [pre_begin[a], pre_begin[a+1]); pre_scale = max |vertex coordinate| of them
+  int32_t n_pre;
+  int32_t pre_begin[4];
+  float pre_scale;
+  int32_t pad2[2];
+  PreQuad pre[kMaxPre];
 };
 
 // camera constants (Camera.cxx:437-474): eye, nlook, delta_x, delta_y
@@ -124,7 +158,7 @@ struct DevCamera {
   float eye[3], nlook[3], dx[3], dy[3];
 };
 
-constexpr int kFfTables = 6;  // jump tables for 32, 16, 8, 4, 2, 1 dead depths
+constexpr int kFfTables = 6;  // jump tables for 32, 16, 8, 4, 2, 1 dead depths (default 4 built)
 
 struct KParams {
   DevCamera cam;

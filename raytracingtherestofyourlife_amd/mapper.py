@@ -351,6 +351,15 @@ class Device:
                                          out.ctypes.data_as(ctypes.c_void_p), a.size))
         return out
 
+    def debug_closest_hit(self, rays: np.ndarray) -> np.ndarray:
+        """(n, 6) float32 rays (o, d) -> (n, 7) uint32: prefiltered (t bits,
+        kind, index), exact scan (t bits, kind, index), fell-back flag."""
+        a = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 6)
+        out = np.zeros((a.shape[0], 7), dtype=np.uint32)
+        check(self._L.rtp_debug_closest_hit(self.handle, a.ctypes.data_as(ctypes.c_void_p), a.shape[0],
+                                            out.ctypes.data_as(ctypes.c_void_p)))
+        return out
+
 
 # ------------------------------------------------------------- mapper --
 class MapperPathTracer:

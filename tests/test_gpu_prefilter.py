@@ -1,0 +1,131 @@
+"""The closest-hit quad prefilter (rtp_kernels.hip closest_hit)
+against the exact scan of every quad, ray by ray (rtp_debug_closest_hit):
+the hit (t bits, primitive kind, index) must be identical for every ray.
+
+The rays are built to sit where an approximate test could go wrong: aimed at
+quad edges and corners with offsets from 0 to a few hundred ulps, leaving
+surfaces (origins on the planes), grazing the planes, parallel to axes (zero
+and negative-zero components), unnormalised, non-finite, far outside the
+margins' coordinate range -- plus the render's own populations (camera rays,
+cosine and light-directed bounces).  The fall-back rate of the ordinary
+populations is also bounded, since a prefilter that falls back often would
+only cost time."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def scene_quads(variant):
+    import raytracingtherestofyourlife_amd as rtp
+
+    cb = rtp.CornellBox(variant)
+    ds = cb.buildDataSet()
+    P = np.asarray(ds.coords, dtype=np.float32).reshape(-1, 3)
+    Q = np.asarray(ds.cellset.quad_points).reshape(-1, 4)
+    return P[Q]  # (nq, 4, 3): v00, v10, v11, v01
+
+
+def stress_rays(verts, n, seed):
+    """(n, 6) float32 rays mixing the hard populations described above."""
+    rng = np.random.default_rng(seed)
+    nq = len(verts)
+    k = n // 8
+    out = []
+    # 1. origins inside the box, aimed at a point on a random quad edge or
+    #    corner, then the target nudged by 0..300 ulps along random axes
+    o = rng.uniform(0.01, 0.99, (k, 3)).astype(np.float32)
+    q = rng.integers(0, nq, k)
+    e = rng.integers(0, 4, k)
+    s = rng.uniform(0, 1, k)
+    s[rng.uniform(0, 1, k) < 0.2] = 0.0  # corners
+    a, b = verts[q, e], verts[q, (e + 1) % 4]
+    tgt = (a + s[:, None] * (b - a)).astype(np.float32)
+    ulps = rng.integers(-300, 301, (k, 3)) * (rng.uniform(0, 1, (k, 3)) < 0.5)
+    tgt = (tgt.view(np.int32) + ulps.astype(np.int32)).view(np.float32)
+    out.append(np.concatenate([o, (tgt - o).astype(np.float32)], 1))
+    # 2. origins ON a quad (the surface a bounce leaves), random directions
+    q = rng.integers(0, nq, k)
+    u, v = rng.uniform(0, 1, (2, k))
+    v00, v10, v01 = verts[q, 0], verts[q, 1], verts[q, 3]
+    o = (v00 + u[:, None] * (v10 - v00) + v[:, None] * (v01 - v00)).astype(np.float32)
+    d = rng.normal(size=(k, 3)).astype(np.float32)
+    out.append(np.concatenate([o, d], 1))
+    # 3. grazing: one direction component tiny (down to denormal) or zero / -0
+    o = rng.uniform(0.01, 0.99, (k, 3)).astype(np.float32)
+    d = rng.normal(size=(k, 3)).astype(np.float32)
+    ax = rng.integers(0, 3, k)
+    tiny = (10.0 ** rng.uniform(-45, -1, k)).astype(np.float32)
+    tiny[rng.uniform(0, 1, k) < 0.2] = 0.0
+    sign = np.where(rng.uniform(0, 1, k) < 0.5, -1.0, 1.0).astype(np.float32)
+    d[np.arange(k), ax] = sign * tiny
+    out.append(np.concatenate([o, d], 1))
+    # 4. origins exactly on a quad's plane but anywhere, and axis-parallel rays
+    o = rng.uniform(-0.2, 1.2, (k, 3)).astype(np.float32)
+    q = rng.integers(0, nq, k)
+    ax = rng.integers(0, 3, k)
+    o[np.arange(k), ax] = verts[q, 0, ax]
+    d = np.zeros((k, 3), np.float32)
+    d[np.arange(k), rng.integers(0, 3, k)] = np.where(rng.uniform(0, 1, k) < 0.5, -1.0, 1.0)
+    mix = rng.uniform(0, 1, k) < 0.5
+    d[mix] = rng.normal(size=(int(mix.sum()), 3)).astype(np.float32)
+    out.append(np.concatenate([o, d], 1))
+    # 5. unnormalised directions (|d| from 1e-4 to 1e3) and origins outside the box
+    o = rng.uniform(-3, 4, (k, 3)).astype(np.float32)
+    d = (rng.normal(size=(k, 3)) * (10.0 ** rng.uniform(-4, 3, (k, 1)))).astype(np.float32)
+    out.append(np.concatenate([o, d], 1))
+    # 6. beyond the margins' range (|o| or |d| > 16) and non-finite components
+    o = rng.uniform(-40, 40, (k, 3)).astype(np.float32)
+    d = rng.normal(size=(k, 3)).astype(np.float32)
+    bad = rng.uniform(0, 1, (k, 6)) < 0.05
+    r = np.concatenate([o, d], 1)
+    r[bad] = rng.choice(np.array([np.nan, np.inf, -np.inf], np.float32), int(bad.sum()))
+    out.append(r)
+    # 7. the render's populations: camera-like rays from the eye, and bounces
+    #    from random surface points toward the light quad
+    eye = np.array([278, 278, -800], np.float32) / np.float32(555)
+    tgt = rng.uniform(0, 1, (k, 3)).astype(np.float32)
+    out.append(np.concatenate([np.broadcast_to(eye, (k, 3)), tgt - eye], 1).astype(np.float32))
+    q = rng.integers(0, nq, k)
+    u, v = rng.uniform(0, 1, (2, k))
+    o = (verts[q, 0] + u[:, None] * (verts[q, 1] - verts[q, 0]) + v[:, None] * (verts[q, 3] - verts[q, 0]))
+    lt = rng.uniform([213, 554, 227], [343, 554, 332], (k, 3)) / 555.0
+    out.append(np.concatenate([o, lt - o], 1).astype(np.float32))
+    return np.ascontiguousarray(np.concatenate(out, 0), dtype=np.float32)
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_gpu_prefilter_equals_exact_scan(device, variant):
+    device.set_cornell_box(variant)
+    verts = scene_quads(variant)
+    rays = stress_rays(verts, 1 << 21, 100 + variant)
+    got = device.debug_closest_hit(rays)
+    bad = np.nonzero((got[:, 0:3] != got[:, 3:6]).any(1))[0]
+    assert bad.size == 0, f"{bad.size} rays differ, first {rays[bad[:3]].tolist()} -> {got[bad[:3]].tolist()}"
+    # the prefilter must actually engage on this scene (axis-plane quads)
+    assert got[:, 6].mean() < 0.5
+
+
+def test_gpu_prefilter_fallback_rate(device):
+    """Camera and bounce rays fall back to the exact scan rarely."""
+    device.set_cornell_box(0)
+    verts = scene_quads(0)
+    rays = stress_rays(verts, 1 << 20, 7)
+    k = len(rays) // 8
+    ordinary = np.concatenate([rays[6 * k:], rays[k:2 * k]])
+    got = device.debug_closest_hit(ordinary)
+    assert (got[:, 0:3] == got[:, 3:6]).all()
+    assert got[:, 6].mean() < 0.01, got[:, 6].mean()
+
+
+def test_gpu_prefilter_bvh_scene_equals_exact(device):
+    """The C3 scene (1000 spheres, BVH kernel variant): quads prefiltered,
+    spheres walked after them, same hit as the exact scan."""
+    device.set_cornell_box(3)
+    verts = scene_quads(3)
+    rays = stress_rays(verts, 1 << 19, 3)
+    got = device.debug_closest_hit(rays)
+    assert (got[:, 0:3] == got[:, 3:6]).all()
+    device.set_cornell_box(0)
