@@ -151,15 +151,29 @@ def main() -> None:
             if rank == 0:
                 canvas.copy_(host)
 
+    # the rank's tiles: computed in the kernel (rtp_render_tiles_device) when
+    # the canvas is whole tiles, else the explicit pixel list
+    tiled = nx % TILE == 0 and ny % TILE == 0 and os.environ.get("RTP_BENCH_LIST") != "1"
+
+    def render():
+        if tiled:
+            dev.render_tiles_device(cam, nx, ny, args.spp, args.depth, out.data_ptr(), rank, world,
+                                    stream=stream.cuda_stream)
+        else:
+            dev.render_device(cam, nx, ny, args.spp, args.depth, out.data_ptr(), pixel_count=npix,
+                              pixel_ids_ptr=ids.data_ptr(), stream=stream.cuda_stream)
+
     def step(count_live: bool = False):
-        dev.render_device(cam, nx, ny, args.spp, args.depth, out.data_ptr(), pixel_count=npix,
-                          pixel_ids_ptr=ids.data_ptr(), stream=stream.cuda_stream,
-                          live_ptr=live.data_ptr() if count_live else 0)
+        if count_live:  # (the list path carries the per-pixel live-bounce counters)
+            dev.render_device(cam, nx, ny, args.spp, args.depth, out.data_ptr(), pixel_count=npix,
+                              pixel_ids_ptr=ids.data_ptr(), stream=stream.cuda_stream, live_ptr=live.data_ptr())
+        else:
+            render()
         canvas.zero_()
         canvas.index_copy_(0, ids, out)
         reduce_canvas()
 
-    for i in range(args.warmup):
+    for i in range(args.warmup):  # the first also counts live bounces (for the byte model)
         step(count_live=(i == 0))
     if args.warmup == 0:
         step(count_live=True)
@@ -174,8 +188,7 @@ def main() -> None:
     for k in range(args.steps):
         # kernel duration bracketed on the stream the kernel is launched on
         ev[k][0].record(stream)
-        dev.render_device(cam, nx, ny, args.spp, args.depth, out.data_ptr(), pixel_count=npix,
-                          pixel_ids_ptr=ids.data_ptr(), stream=stream.cuda_stream)
+        render()
         ev[k][1].record(stream)
         canvas.zero_()
         canvas.index_copy_(0, ids, out)
@@ -238,7 +251,7 @@ def main() -> None:
             "config": {
                 "workload": "C2: Cornell Box 800x800 per GPU, 1000 spp, depth 50",
                 "nx": nx, "ny": ny, "spp": args.spp, "depth": args.depth,
-                "pixels_per_gpu": npix, "shard": f"{TILE}x{TILE} tiles round-robin, 1 RCCL reduce/step",
+                "pixels_per_gpu": npix, "shard": f"{TILE}x{TILE} tiles round-robin (" + ("pixel of each tile entry computed in-kernel" if tiled else "pixel list") + "), 1 RCCL reduce/step",
                 "live_bounces_per_sample": round(L, 6),
             },
             "roofline": {

@@ -120,6 +120,16 @@ rtp_status rtp_set_scene(rtp_context* ctx, const rtp_scene_desc* scene);
 rtp_status rtp_render(rtp_context* ctx, const rtp_camera* cam, int32_t nx, int32_t ny, int32_t spp,
                       int32_t depth, uint32_t seed_base, float* rgba_out, rtp_stats* stats);
 
+/* rtp_render_device over the 16x16 tiles of a round-robin tile deal: rank
+ * `rank` of `world` owns tiles t = rank, rank + world, ... of the canvas in
+ * row-major tile order, each tile's pixels row-major (the order of
+ * shard.tile_pixels; the multi-GPU sharding of SURVEY.md 8(e)).
+ * d_rgba_out: device float4[256 * tiles owned].  nx and ny must be multiples
+ * of 16.  Equal to rtp_render_device with that pixel list, without the list. */
+rtp_status rtp_render_tiles_device(rtp_context* ctx, const rtp_camera* cam, int32_t nx, int32_t ny, int32_t spp,
+                                   int32_t depth, uint32_t seed_base, int32_t rank, int32_t world, float* d_rgba_out,
+                                   void* hip_stream, rtp_stats* stats);
+
 /* Device-resident render of a pixel set on hip_stream (0 = null stream).
  * Pixels: d_pixel_ids (device int64[pixel_count]) when non-NULL, else the
  * contiguous range [pixel_begin, pixel_begin+pixel_count).  d_rgba_out is a

@@ -62,7 +62,7 @@ RTP_AOV_COLOR, RTP_AOV_NORMALS, RTP_AOV_ALBEDO = 1, 2, 4
 
 EXPORTED_SYMBOLS = [
     "rtp_last_error", "rtp_abi_version", "rtp_create", "rtp_destroy", "rtp_set_scene", "rtp_render",
-    "rtp_render_device", "rtp_render_pixels", "rtp_normalize", "rtp_write_pnm", "rtp_cornell_box",
+    "rtp_render_device", "rtp_render_tiles_device", "rtp_render_pixels", "rtp_normalize", "rtp_write_pnm", "rtp_cornell_box",
     "rtp_eval_primitive", "rtp_debug_counters", "rtp_verify_fast_math", "rtp_debug_closest_hit",
     "rtp_render_direct", "rtp_render_direct_device", "rtp_sample_color_table", "rtp_quad_scalars",
     "rtp_cornell_point_field", "rtp_write_pnm_depth", "rtp_eval_powf",
@@ -110,6 +110,9 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
                                     ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_int64,
                                     ctypes.c_int64, vp, vp, ctypes.POINTER(RtpPixelAux), vp,
                                     ctypes.POINTER(RtpStats)]
+    L.rtp_render_tiles_device.argtypes = [vp, ctypes.POINTER(RtpCamera), ctypes.c_int32, ctypes.c_int32,
+                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_int32,
+                                          ctypes.c_int32, vp, vp, ctypes.POINTER(RtpStats)]
     L.rtp_render_pixels.argtypes = [vp, ctypes.POINTER(RtpCamera), ctypes.c_int32, ctypes.c_int32,
                                     ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, i64p, ctypes.c_int64, f32p,
                                     ctypes.POINTER(RtpPixelAux), ctypes.POINTER(RtpStats)]

@@ -747,9 +747,11 @@ rtp_status ensure_hist(rtp_context* c, size_t bytes) {
 
 rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny, int32_t spp, int32_t depth,
                   uint32_t seed_base, int64_t pixel_begin, int64_t npix, const int64_t* d_ids, float* d_out,
-                  uint32_t* d_seed, uint32_t* d_live, hipStream_t stream, double* kernel_ms) {
+                  uint32_t* d_seed, uint32_t* d_live, hipStream_t stream, double* kernel_ms,
+                  const int32_t* tile = nullptr) {
   HIP_TRY(hipSetDevice(c->device));
   rtp::KParams p{};
+  if (tile) p.tile_tx = tile[0], p.tile_world = tile[1], p.tile_rank = tile[2];
   camera_setup(cam, nx, ny, &p.cam);
   p.nx = nx, p.ny = ny, p.spp = spp, p.depth = depth;
   p.seed_base = seed_base;
@@ -898,6 +900,36 @@ rtp_status rtp_render_device(rtp_context* c, const rtp_camera* cam, int32_t nx, 
               stats ? &ms : nullptr);
   if (rs == RTP_OK && stats) {
     stats->samples = (uint64_t)pixel_count * (uint64_t)spp;
+    stats->live_bounces = 0;
+    stats->nan_pixels = 0;
+    stats->kernel_ms = ms;
+  }
+  return rs;
+}
+
+// rtp_render_device over the rank's tiles of a round-robin 16x16 tile deal
+// (shard.tile_pixels) without a pixel list: the kernel computes each entry's
+// pixel, which saves the per-sample gather of its id.
+rtp_status rtp_render_tiles_device(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny, int32_t spp,
+                                   int32_t depth, uint32_t seed_base, int32_t rank, int32_t world, float* d_rgba_out,
+                                   void* hip_stream, rtp_stats* stats) {
+  rtp_status rs = check_render_args(c, cam, nx, ny, spp, depth);
+  if (rs != RTP_OK) return rs;
+  if (nx % 16 != 0 || ny % 16 != 0)
+    return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_render_tiles_device: nx and ny must be multiples of 16");
+  if (world < 1 || rank < 0 || rank >= world)
+    return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_render_tiles_device: rank outside [0, world)");
+  const int64_t tiles = (int64_t)(nx / 16) * (ny / 16);
+  if (tiles >= (1 << 24)) return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_render_tiles_device: canvas too large");
+  const int64_t mine = tiles / world + (rank < tiles % world ? 1 : 0);
+  if (mine == 0) return RTP_OK;
+  if (!d_rgba_out) return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_render_tiles_device: bad output");
+  const int32_t tile[3] = {nx / 16, world, rank};
+  double ms = 0;
+  rs = launch(c, cam, nx, ny, spp, depth, seed_base, 0, mine * 256, nullptr, d_rgba_out, nullptr, nullptr,
+              (hipStream_t)hip_stream, stats ? &ms : nullptr, tile);
+  if (rs == RTP_OK && stats) {
+    stats->samples = (uint64_t)mine * 256 * (uint64_t)spp;
     stats->live_bounces = 0;
     stats->nan_pixels = 0;
     stats->kernel_ms = ms;

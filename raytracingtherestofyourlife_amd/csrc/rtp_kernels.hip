@@ -694,7 +694,24 @@ RTP_DEV f3 path_radiance(int result, int k, f3 emit, bool nonfinite, const float
   return mk(sx, sy, sz);
 }
 
-RTP_DEV int64_t pixel_of(const KParams& p, int64_t k) { return p.pixel_ids ? p.pixel_ids[k] : p.pixel_begin + k; }
+// Tile-deal index arithmetic: q = ti / tx from a float reciprocal, then one
+// correction each way (ti < 2^24, so the estimate is off by at most one).
+RTP_DEV int64_t tile_pixel(const KParams& p, int64_t k) {
+  const int ti = (int)(k >> 8) * p.tile_world + p.tile_rank, within = (int)(k & 255);
+  int ty = (int)((float)ti * __builtin_amdgcn_rcpf((float)p.tile_tx));
+  ty += (ty + 1) * p.tile_tx <= ti;
+  ty -= ty * p.tile_tx > ti;
+  const int tx = ti - ty * p.tile_tx;
+  return (int64_t)(ty * 16 + (within >> 4)) * p.nx + tx * 16 + (within & 15);
+}
+// kTiles: a separate kernel instance (rtp_render_tiles_device).  A runtime
+// branch here changed the compiler's code for the whole scheduling loop of
+// the other modes (+9% time), as other additions to the refill path did.
+template <bool kTiles = false>
+RTP_DEV int64_t pixel_of(const KParams& p, int64_t k) {
+  if constexpr (kTiles) return tile_pixel(p, k);
+  else return p.pixel_ids ? p.pixel_ids[k] : p.pixel_begin + k;
+}
 
 // ------------------------------------------------------------------ v1 ---
 template <bool kBvh>
@@ -796,7 +813,7 @@ RTP_DEV void set_priority(float lag) {  // s_setprio needs an immediate
 #ifndef RTP_POOL_MAX_VGPR
 #define RTP_POOL_MAX_VGPR 96
 #endif
-template <bool kStats, bool kBvh>
+template <bool kStats, bool kBvh, bool kTiles = false>
 #if RTP_POOL_MAX_VGPR > 0
 #define RTP_POOL_VGPR_ATTR __attribute__((amdgpu_num_vgpr(RTP_POOL_MAX_VGPR)))
 #else
@@ -833,7 +850,7 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
   const int n_slots = left <= 0 ? 0 : (int)min<int64_t>(kPool, (left + n_waves - 1) / n_waves);
   for (int j = lane; j < n_slots; j += 64) {
     const int64_t k = (int64_t)j * n_waves + w;
-    s_seed[j] = p.seed_base + (uint32_t)pixel_of(p, k);  // seeds[i] = i (MapperPathTracer.cxx:265-267)
+    s_seed[j] = p.seed_base + (uint32_t)pixel_of<kTiles>(p, k);  // seeds[i] = i (MapperPathTracer.cxx:265-267)
     s_r[j] = 0.f;
     s_g[j] = 0.f;
     s_b[j] = 0.f;
@@ -1004,7 +1021,7 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
 #if RTP_DEFER_RADIANCE
         hist = hist_base + slot;
 #endif
-        const int64_t pix = pixel_of(p, (int64_t)slot * n_waves + w);
+        const int64_t pix = pixel_of<kTiles>(p, (int64_t)slot * n_waves + w);
         const int pi = (int32_t)pix % p.nx, pj = (int32_t)pix / p.nx;
         ps.dir = camera_ray(p.cam, pi, pj, p.nx, p.ny, seed);
 #if RTP_DUP == 7
@@ -1273,6 +1290,7 @@ extern "C" hipError_t rtp_launch_eval_closest(const rtp::DevScene* scene, const 
 extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::KParams* p, int variant, int waves,
                                         int bvh, hipStream_t stream) {
   if (p->npix <= 0) return hipSuccess;
+  if (variant == 1 && p->tile_world > 0) return hipErrorNotSupported;  // (v1 takes pixel lists or ranges)
   if (variant == 1) {
     const int64_t grid = (p->npix + 255) / 256;
     if (bvh)
@@ -1284,7 +1302,10 @@ extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::K
     const char* st = getenv("RTP_DEBUG_STATS");
     const bool stats = p->dbg && st && st[0] == '1';
     const dim3 g((unsigned)blocks), b(256);
-    if (stats && bvh) hipLaunchKernelGGL((rtp::rtp_render_pool<true, true>), g, b, 0, stream, scene, *p, waves);
+    if (p->tile_world > 0) {  // the tile deal: its own instances, no stats variant
+      if (bvh) hipLaunchKernelGGL((rtp::rtp_render_pool<false, true, true>), g, b, 0, stream, scene, *p, waves);
+      else hipLaunchKernelGGL((rtp::rtp_render_pool<false, false, true>), g, b, 0, stream, scene, *p, waves);
+    } else if (stats && bvh) hipLaunchKernelGGL((rtp::rtp_render_pool<true, true>), g, b, 0, stream, scene, *p, waves);
     else if (stats) hipLaunchKernelGGL((rtp::rtp_render_pool<true, false>), g, b, 0, stream, scene, *p, waves);
     else if (bvh) hipLaunchKernelGGL((rtp::rtp_render_pool<false, true>), g, b, 0, stream, scene, *p, waves);
     else hipLaunchKernelGGL((rtp::rtp_render_pool<false, false>), g, b, 0, stream, scene, *p, waves);

@@ -166,6 +166,10 @@ struct KParams {
   uint32_t seed_base;
   int64_t pixel_begin;
   const int64_t* pixel_ids;  // nullable
+  // tile deal (tile_world > 0, pixel_ids null): entry k is pixel (k & 255) of
+  // the rank's (k >> 8)-th 16x16 tile, tiles dealt round-robin in row-major
+  // order over a canvas of tile_tx tiles per row (shard.tile_pixels' order)
+  int32_t tile_tx, tile_world, tile_rank, tile_pad;
   int64_t npix;
   float* out;                // float4[npix]
   uint32_t* seed_out;        // nullable

@@ -311,6 +311,17 @@ class Device:
                                         ctypes.byref(st) if timed else None))
         return st
 
+    def render_tiles_device(self, camera: Camera, nx: int, ny: int, spp: int, depth: int, out_ptr: int,
+                            rank: int, world: int, seed_base: int = 0, stream: int = 0, timed: bool = False):
+        """Device-resident render of rank's tiles of the round-robin 16x16
+        tile deal (out_ptr: device float4[256 * tiles], shard.tile_pixels order)."""
+        st = RtpStats()
+        cam = camera.to_c()
+        check(self._L.rtp_render_tiles_device(self.handle, ctypes.byref(cam), nx, ny, spp, depth, seed_base, rank,
+                                              world, ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream or None),
+                                              ctypes.byref(st) if timed else None))
+        return st
+
     DEBUG_COUNTERS = ("bounce_steps", "bounce_lanes", "ff_phases", "ff_lanes", "ff_iters", "cycles_bounce",
                       "cycles_ff", "cycles_total", "cycles_intersect", "cycles_bounce_call", "cycles_end",
                       "cycles_refill", "real_start", "real_end", "hw_id", "tail_steps", "tail_lanes",

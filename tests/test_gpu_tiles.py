@@ -1,0 +1,44 @@
+"""rtp_render_tiles_device (the tile deal computed in the kernel) against
+rtp_render_device with shard.tile_pixels' explicit list: bit-identical
+output, entry for entry, for every rank of several deals."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("nx,ny,world", [(64, 48, 1), (64, 48, 2), (80, 32, 3), (48, 64, 5)])
+def test_gpu_tile_deal_equals_pixel_list(device, nx, ny, world):
+    import torch
+
+    import raytracingtherestofyourlife_amd as rtp
+    from raytracingtherestofyourlife_amd import shard
+
+    device.set_cornell_box(0)
+    cam = rtp.default_camera()
+    s = torch.cuda.current_stream().cuda_stream
+    for rank in range(world):
+        ids_np = shard.tile_pixels(nx, ny, rank, world)
+        ids = torch.from_numpy(ids_np).cuda()
+        a = torch.full((ids_np.size, 4), 7.0, dtype=torch.float32, device="cuda")
+        b = torch.full((ids_np.size, 4), 9.0, dtype=torch.float32, device="cuda")
+        device.render_device(cam, nx, ny, 5, 10, a.data_ptr(), pixel_count=ids_np.size, pixel_ids_ptr=ids.data_ptr(),
+                             stream=s)
+        device.render_tiles_device(cam, nx, ny, 5, 10, b.data_ptr(), rank, world, stream=s)
+        torch.cuda.synchronize()
+        an, bn = a.cpu().numpy(), b.cpu().numpy()
+        assert np.array_equal(an.view(np.uint32), bn.view(np.uint32)), (nx, ny, world, rank)
+
+
+def test_gpu_tile_deal_rejects_partial_tiles(device):
+    import torch
+
+    import raytracingtherestofyourlife_amd as rtp
+
+    out = torch.empty((256, 4), dtype=torch.float32, device="cuda")
+    with pytest.raises(Exception):
+        device.render_tiles_device(rtp.default_camera(), 40, 32, 1, 5, out.data_ptr(), 0, 1)
+    with pytest.raises(Exception):
+        device.render_tiles_device(rtp.default_camera(), 32, 32, 1, 5, out.data_ptr(), 2, 2)
