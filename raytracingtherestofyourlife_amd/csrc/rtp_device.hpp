@@ -326,9 +326,8 @@ RTP_DEV f2v dot_m2l(const float* x, const f2v (&y)[3]) {  // dot_m with a shared
   else return f2v{0.0f, 0.0f};
 }
 
-// QT: DevQuad, or QuadTest (the same leading fields; an LDS copy)
-template <int K, class QT = DevQuad>
-RTP_DEV bool quad_hit_masked(const QT& Q, f3 o, f3 d, float& t_out) {
+template <int K>
+RTP_DEV bool quad_hit_masked(const DevQuad& Q, f3 o, f3 d, float& t_out) {
   constexpr int M01 = kQuadKind[K].m01, M03 = kQuadKind[K].m03, M21 = kQuadKind[K].m21, M23 = kQuadKind[K].m23;
   constexpr int MP = cross_mask(M03), MQ = cross_mask(M01), MPp = cross_mask(M21), MQp = cross_mask(M23);
   const float dv[3] = {d.x, d.y, d.z};

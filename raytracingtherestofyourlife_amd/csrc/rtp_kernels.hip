@@ -228,28 +228,13 @@ RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
 
 // qshade: the block's LDS copy of the quads' shading data (n, alb, mt) so
 // the hit's material is an LDS gather instead of a global one.
-// Each record: n, alb, mt, pad (8 words); with RTP_PRE_LDS the QuadTest copy
-// (24 words) for the prefilter's per-lane exact test follows.
-#ifndef RTP_PRE_LDS
-#define RTP_PRE_LDS 0
-#endif
-constexpr int kLdsQuads = 64, kQTestOffset = 8, kQShadeFloats = RTP_PRE_LDS ? 32 : 8;
-static_assert(!RTP_PRE_LDS || kQTestOffset + sizeof(QuadTest) / 4 == kQShadeFloats, "qshade record layout");
+constexpr int kLdsQuads = 64, kQShadeFloats = 8;  // per quad: n, alb, mt, pad
 
-// The block's LDS copy of the quads' shading data and QuadTest records.
 RTP_DEV void fill_qshade(const DevScene* __restrict__ sc, float* s_qshade) {
   for (int i = threadIdx.x; i < sc->n_quads * kQShadeFloats; i += blockDim.x) {
     const DevQuad& Q = sc->quads[i / kQShadeFloats];
-    const int f = i % kQShadeFloats, g = f - kQTestOffset;
-    const float* qw = reinterpret_cast<const float*>(&Q);
-    s_qshade[i] = f < 3                                        ? Q.n[f]
-                  : f < 6                                      ? Q.alb[f - 3]
-                  : f == 6                                     ? __int_as_float(Q.mt)
-                  : f < kQTestOffset                           ? 0.f
-                  : g < (int)(offsetof(QuadTest, para) / 4)    ? qw[g]
-                  : g == (int)(offsetof(QuadTest, para) / 4)   ? __int_as_float(Q.para)
-                  : g == (int)(offsetof(QuadTest, key_lo) / 4) ? __uint_as_float(Q.key_lo)
-                                                               : 0.f;
+    const int f = i % kQShadeFloats;
+    s_qshade[i] = f < 3 ? Q.n[f] : f < 6 ? Q.alb[f - 3] : f == 6 ? __int_as_float(Q.mt) : 0.f;
   }
 }
 
@@ -378,11 +363,7 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, const float
     pre_axis<1>(sc, o, d, ma, mb, k1, k2);
     pre_axis<2>(sc, o, d, ma, mb, k1, k2);
     if (lane_ok && k1 != ~0u) {  // (finite o, d: the generic arithmetic equals the kind's)
-#if RTP_PRE_LDS
-      const QuadTest& Q = *reinterpret_cast<const QuadTest*>(qshade + (k1 & 31u) * kQShadeFloats + kQTestOffset);
-#else
-      const DevQuad& Q = sc->quads[k1 & 31u];  // a per-lane (vector) load: measured faster than the LDS copy
-#endif
+      const DevQuad& Q = sc->quads[k1 & 31u];  // a per-lane (vector) load: measured faster than an LDS copy
       float t;
       const bool ok = quad_hit_masked<0>(Q, o, d, t);
       const uint64_t kq = (uint64_t)__float_as_uint(t) << 32 | Q.key_lo;

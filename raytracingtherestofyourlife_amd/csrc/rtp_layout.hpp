@@ -56,18 +56,6 @@ struct alignas(16) DevQuad {
   int32_t pad[3];
 };
 
-// The fields of DevQuad the Lagae-Dutre test reads, plus its hit-key word:
-// the pool kernel's LDS copy for the prefilter's per-lane exact test.
-struct alignas(16) QuadTest {
-  float vv[3][2];
-  float e01[3], e03[3];
-  float e21[3], e23[3];
-  int32_t para;
-  uint32_t key_lo;
-  int32_t pad[4];
-};
-static_assert(offsetof(DevQuad, e23) == offsetof(QuadTest, e23), "QuadTest leads like DevQuad");
-
 struct alignas(16) DevSphere {
   float c[3];
   float r;
