@@ -7,7 +7,8 @@ One step = one full render of the C2 workload on every rank: Cornell Box,
 N > 1 (launched by torch.distributed.run, one process per GPU): weak scaling
 by image tiles -- the canvas is 800 x (800*N), 16x16 tiles are dealt to the
 ranks round-robin (every rank renders 640,000 pixels), and the float4
-framebuffer is summed to rank 0 with ONE RCCL reduce per step (exact: every
+framebuffer is summed to rank 0 with ONE RCCL reduce per step, overlapped with
+the next step's render (two canvases, alternating; exact: every
 pixel is non-zero on exactly one rank).
 
 Rank 0 prints one JSON line.  `value` = all ranks' samples / max-over-ranks
@@ -140,16 +141,16 @@ def main() -> None:
     live = torch.zeros(npix, dtype=torch.int32, device="cuda")
     stream = torch.cuda.current_stream()
 
-    def reduce_canvas():
-        if world == 1:
-            return
-        if args.dist_backend == "nccl":
-            dist.reduce(canvas, dst=0, op=dist.ReduceOp.SUM)
-        else:  # gloo reduces host tensors
-            host = canvas.cpu()
-            dist.reduce(host, dst=0, op=dist.ReduceOp.SUM)
-            if rank == 0:
-                canvas.copy_(host)
+    # RCCL: the reduce of step k runs on the collective stream while step k+1
+    # renders (shard.OverlappedCanvasReduce); gloo reduces host tensors.
+    red = shard.OverlappedCanvasReduce(canvas, dist, overlap=(args.dist_backend == "nccl"),
+                                       host_copy=(args.dist_backend != "nccl"))
+
+    def gather_canvas():
+        return red.step(ids, out)
+
+    def drain():
+        red.drain()
 
     # the rank's tiles: computed in the kernel (rtp_render_tiles_device) when
     # the canvas is whole tiles, else the explicit pixel list
@@ -169,14 +170,13 @@ def main() -> None:
                               pixel_ids_ptr=ids.data_ptr(), stream=stream.cuda_stream, live_ptr=live.data_ptr())
         else:
             render()
-        canvas.zero_()
-        canvas.index_copy_(0, ids, out)
-        reduce_canvas()
+        return gather_canvas()
 
     for i in range(args.warmup):  # the first also counts live bounces (for the byte model)
         step(count_live=(i == 0))
     if args.warmup == 0:
         step(count_live=True)
+    drain()
     torch.cuda.synchronize()
     live_total = int(live.to(torch.int64).sum().item())
 
@@ -190,9 +190,8 @@ def main() -> None:
         ev[k][0].record(stream)
         render()
         ev[k][1].record(stream)
-        canvas.zero_()
-        canvas.index_copy_(0, ids, out)
-        reduce_canvas()
+        canvas = gather_canvas()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -89,6 +89,54 @@ def reduce_canvas(canvas, dist) -> None:
         dist.reduce(canvas, dst=0, op=dist.ReduceOp.SUM)
 
 
+class OverlappedCanvasReduce:
+    """The per-step canvas reduce of bench.py, overlapped with the next
+    step: the rank's entries are scattered into one of two canvases, whose
+    reduce (async) runs while the next step renders; a canvas is reused only
+    after its reduce has been waited on.  overlap=False: one canvas, a
+    synchronous reduce (gloo reduces host tensors: `host_copy` moves a device
+    canvas through the host)."""
+
+    def __init__(self, canvas, dist, overlap: bool, host_copy: bool = False):
+        import torch
+
+        self.dist, self.overlap, self.host_copy = dist, overlap, host_copy
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self.canvases = [canvas, torch.zeros_like(canvas)] if overlap and self.world > 1 else [canvas]
+        self.pending = [None] * len(self.canvases)
+        self.steps = 0
+
+    def step(self, ids, part):
+        """Zero the next canvas, scatter `part` at `ids`, start its reduce;
+        returns that canvas (rank 0 holds the sum once drained)."""
+        slot = self.steps % len(self.canvases)
+        self.steps += 1
+        if self.pending[slot] is not None:
+            self.pending[slot].wait()
+            self.pending[slot] = None
+        c = self.canvases[slot]
+        c.zero_()
+        c.index_copy_(0, ids, part)
+        if self.world > 1:
+            if len(self.canvases) > 1:
+                self.pending[slot] = self.dist.reduce(c, dst=0, op=self.dist.ReduceOp.SUM, async_op=True)
+            elif self.host_copy:
+                host = c.cpu()
+                self.dist.reduce(host, dst=0, op=self.dist.ReduceOp.SUM)
+                if self.rank == 0:
+                    c.copy_(host)
+            else:
+                self.dist.reduce(c, dst=0, op=self.dist.ReduceOp.SUM)
+        return c
+
+    def drain(self) -> None:
+        for i, w in enumerate(self.pending):
+            if w is not None:
+                w.wait()
+                self.pending[i] = None
+
+
 def _as_like(canvas, a):
     if isinstance(canvas, np.ndarray):
         return np.asarray(a, dtype=np.float32)

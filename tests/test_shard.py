@@ -113,3 +113,40 @@ def test_sample_shards_reduce_to_summed_shards(tmp_path):
     parts = [render(None, b.spp, b.seed_base) for b in shard.sample_batches(SPP, 2, NX * NY)]
     want = parts[0] + parts[1]
     assert _same(got[:, :3], want[:, :3])
+
+
+def _overlap_worker(rank, world, port, overlap, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from raytracingtherestofyourlife_amd import shard
+
+    n = 64
+    canvas = torch.zeros((n, 4), dtype=torch.float32)
+    red = shard.OverlappedCanvasReduce(canvas, dist, overlap=overlap)
+    ids = torch.arange(rank, n, world)
+    last = None
+    for step in range(5):
+        part = torch.full((ids.numel(), 4), float(100 * step + rank + 1))
+        last = red.step(ids, part)
+    red.drain()
+    if rank == 0:
+        np.save(out_path, last.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_overlapped_canvas_reduce(tmp_path, overlap):
+    """bench.py's per-step reduce, async on two alternating canvases (the
+    RCCL path, here with gloo's async reduce) or synchronous on one: rank 0
+    ends with the last step's entries of every rank, nothing left over from
+    earlier steps."""
+    world = 2
+    out = str(tmp_path / "ov.npy")
+    mp.start_processes(_overlap_worker, args=(world, _free_port(), overlap, out), nprocs=world, join=True,
+                       start_method="spawn")
+    got = np.load(out)
+    want = np.zeros((64, 4), np.float32)
+    for r in range(world):
+        want[r::world] = 100 * 4 + r + 1
+    assert np.array_equal(got, want)
