@@ -46,9 +46,6 @@
 #ifndef RTP_FAIR_READY
 #define RTP_FAIR_READY 1  // pool kernel: lagging pixels jump the READY queue
 #endif
-#ifndef RTP_QSHADE_LDS
-#define RTP_QSHADE_LDS 1  // pool kernel: quads' shading data gathered from LDS
-#endif
 #ifndef RTP_DEFER_RADIANCE
 #define RTP_DEFER_RADIANCE 1  // pool kernel: radiance product in the fast-forward batch
 #endif
@@ -228,7 +225,10 @@ RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
 
 // qshade: the block's LDS copy of the quads' shading data (n, alb, mt) so
 // the hit's material is an LDS gather instead of a global one.
-constexpr int kLdsQuads = 64, kQShadeFloats = 8;  // per quad: n, alb, mt, pad
+// Every quad of a scene (kMaxQuads, 8 KiB): with a table that could be
+// absent, the compiler merged the LDS and global reads of the hit's record
+// into 7 flat loads (waited on both counters); now they are 2 ds_read_b128.
+constexpr int kLdsQuads = kMaxQuads, kQShadeFloats = 8;  // per quad: n, alb, mt, pad
 
 RTP_DEV void fill_qshade(const DevScene* __restrict__ sc, float* s_qshade) {
   for (int i = threadIdx.x; i < sc->n_quads * kQShadeFloats; i += blockDim.x) {
@@ -308,7 +308,7 @@ RTP_DEV void pre_axis(const DevScene* __restrict__ sc, f3 o, f3 d, float ma, flo
 }
 
 template <bool kBvh>
-RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, const float* qshade = nullptr,
+RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefilter = false,
                         uint32_t* full_out = nullptr) {
   Hit h{3.40282347e+38f, -1, 0};
   int best = 0x7fffffff;
@@ -350,7 +350,7 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, const float
   scan_kind<0>(sc, 10, o, d, key);
   bool full = true;  // this lane needs the exact scan of the axis-plane quads (kinds 1..6)
 #if RTP_PREFILTER
-  const bool pre = qshade != nullptr && sc->n_pre > 0;  // wave-uniform
+  const bool pre = prefilter && sc->n_pre > 0;  // wave-uniform
   if (pre) {
     const bool lane_ok = (int)(fabsf(o.x) <= kPreLimD) & (int)(fabsf(o.y) <= kPreLimD) &
                          (int)(fabsf(o.z) <= kPreLimD) & (int)(fabsf(d.x) <= kPreLimD) &
@@ -363,7 +363,10 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, const float
     pre_axis<1>(sc, o, d, ma, mb, k1, k2);
     pre_axis<2>(sc, o, d, ma, mb, k1, k2);
     if (lane_ok && k1 != ~0u) {  // (finite o, d: the generic arithmetic equals the kind's)
-      const DevQuad& Q = sc->quads[k1 & 31u];  // a per-lane (vector) load: measured faster than an LDS copy
+      // a per-lane load: measured faster than an LDS copy.  Through a global
+      // (address space 1) pointer: the generic one compiled to flat loads.
+      const auto* gq = (const __attribute__((address_space(1))) DevQuad*)(sc->quads);
+      const DevQuad& Q = *(const DevQuad*)(gq + (k1 & 31u));
       float t;
       const bool ok = quad_hit_masked<0>(Q, o, d, t);
       const uint64_t kq = (uint64_t)__float_as_uint(t) << 32 | Q.key_lo;
@@ -452,11 +455,10 @@ RTP_DEV unsigned long long stamp(bool on) { return on ? __builtin_amdgcn_s_memti
 // kDeferDead: a path that misses or hits the light at depth k leaves its
 // depth-k draws (which + generator, exactly one dead step) to the caller's
 // fast-forward instead of drawing them here.
-// qshade (nullable): the block's LDS quad table (fill_qshade); also turns
-// on the closest-hit prefilter.
+// qshade: the block's LDS quad table (fill_qshade).
 template <bool kBvh, bool kDeferDead = false>
 RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3& emit, float4* __restrict__ hist_d,
-                   int D, unsigned long long* dbg = nullptr, const float* qshade = nullptr) {
+                   int D, unsigned long long* dbg, const float* qshade) {
   const bool st = dbg != nullptr;
   const unsigned long long t0 = stamp(st);
   const uint32_t t1 = sc->which_t1, t2 = sc->which_t2;
@@ -464,7 +466,7 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
   const f3 org = ps.org, dir = ps.dir;
   const int d = ps.d;
   // intersect + CollectIntersecttWorklet (SurfaceWorklets.h:104-109)
-  Hit h = closest_hit<kBvh>(sc, org, dir, qshade);
+  Hit h = closest_hit<kBvh>(sc, org, dir, true);
 #if RTP_DUP == 1
   {
     f3 o2 = org;
@@ -486,17 +488,13 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
   int mt;
   f3 alb;
   if (h.kind == 0) {
-    if (qshade != nullptr) {
-      const float* r = qshade + h.idx * kQShadeFloats;
-      hn = mk(r[0], r[1], r[2]);
-      alb = mk(r[3], r[4], r[5]);
-      mt = __float_as_int(r[6]);
-    } else {
-      const DevQuad& Q = sc->quads[h.idx];
-      hn = ld3(Q.n);
-      mt = Q.mt;
-      alb = ld3(Q.alb);
-    }
+    // (an LDS table always: a global fallback here made the compiler read
+    // both through one flat pointer)
+    const float4* r = reinterpret_cast<const float4*>(qshade + h.idx * kQShadeFloats);  // 16-byte aligned
+    const float4 r0 = r[0], r1 = r[1];
+    hn = mk(r0.x, r0.y, r0.z);
+    alb = mk(r0.w, r1.x, r1.y);
+    mt = __float_as_int(r1.z);
     if (dot(hn, dir) > 0.f) hn = neg(hn);  // Surface.h:184-185
   } else {
     const DevSphere& S = kBvh ? sc->sph_all[h.idx] : sc->spheres[h.idx];
@@ -697,6 +695,9 @@ RTP_DEV int64_t pixel_of(const KParams& p, int64_t k) {
 // ------------------------------------------------------------------ v1 ---
 template <bool kBvh>
 __global__ void __launch_bounds__(256) rtp_render_lockstep(const DevScene* __restrict__ sc, KParams p) {
+  __shared__ __align__(16) float s_qshade[kLdsQuads * kQShadeFloats];
+  fill_qshade(sc, s_qshade);
+  __syncthreads();
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= p.npix) return;
   const int64_t pix = pixel_of(p, k);
@@ -722,7 +723,7 @@ __global__ void __launch_bounds__(256) rtp_render_lockstep(const DevScene* __res
       }
       live++;
       ps.d = d;
-      result = bounce<kBvh>(sc, ps, seed, emit, hist + (int64_t)d * stride, D);
+      result = bounce<kBvh>(sc, ps, seed, emit, hist + (int64_t)d * stride, D, nullptr, s_qshade);
       if (result != kAlive) k_end = d;
     }
     f3 c = path_radiance(result, k_end, emit, ps.nonfinite, hist, stride);
@@ -802,15 +803,12 @@ template <bool kStats, bool kBvh, bool kTiles = false>
 #endif
 __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_ATTR rtp_render_pool(const DevScene* __restrict__ sc, KParams p, int n_waves) {
   __shared__ __align__(16) unsigned char smem[kPoolLdsBytes + RTP_LDS_PAD];
-  __shared__ float s_qshade[kLdsQuads * kQShadeFloats];
+  __shared__ __align__(16) float s_qshade[kLdsQuads * kQShadeFloats];
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
   const int w = blockIdx.x * kWavesPerBlock + wib;  // global wave id
   // the quads' shading data into LDS (the block's only barrier, before any wave leaves)
-  const bool qshade_lds = RTP_QSHADE_LDS && sc->n_quads <= kLdsQuads;
-  if (qshade_lds) {
-    fill_qshade(sc, s_qshade);
-  }
+  fill_qshade(sc, s_qshade);  // (n_quads <= kMaxQuads = kLdsQuads)
   __syncthreads();
   if (w >= n_waves) return;  // whole wave leaves; no block-level barriers follow
   unsigned char* base = smem + (size_t)wib * kPool * kSlotBytes;
@@ -1029,7 +1027,7 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
     if (has_path) {
       f3 emit = mk(0.f, 0.f, 0.f);
       const int res = bounce<kBvh, true>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D, want_dbg ? dbg : nullptr,
-                                         qshade_lds ? s_qshade : nullptr);
+                                         s_qshade);
       tbnc = stamp(want_dbg);
       if (res == kAlive && ps.d < D - 1) {
         ps.d++;
@@ -1139,16 +1137,15 @@ template <bool kBvh>
 __global__ void __launch_bounds__(256) rtp_eval_closest_kernel(const DevScene* __restrict__ sc,
                                                                const float* __restrict__ rays, uint32_t* out,
                                                                int64_t n) {
-  __shared__ float s_qshade[kLdsQuads * kQShadeFloats];
-  const bool lds = sc->n_quads <= kLdsQuads;
-  if (lds) fill_qshade(sc, s_qshade);
+  __shared__ __align__(16) float s_qshade[kLdsQuads * kQShadeFloats];
+  fill_qshade(sc, s_qshade);
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float* r = rays + 6 * i;
   const f3 o = mk(r[0], r[1], r[2]), d = mk(r[3], r[4], r[5]);
   uint32_t full = 0;
-  const Hit a = closest_hit<kBvh>(sc, o, d, lds ? s_qshade : nullptr, &full);
+  const Hit a = closest_hit<kBvh>(sc, o, d, true, &full);
   const Hit b = closest_hit<kBvh>(sc, o, d);
   uint32_t* w = out + 7 * i;
   w[0] = __float_as_uint(a.t), w[1] = (uint32_t)a.kind, w[2] = (uint32_t)a.idx;
