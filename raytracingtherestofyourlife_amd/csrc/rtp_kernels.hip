@@ -155,8 +155,19 @@ RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
   const int nn = sc->n_nodes;
   // the copy of the tree ordered near-to-far for this ray's direction octant
   const int oct = (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0);
-  const float4* __restrict__ nodes = reinterpret_cast<const float4*>(sc->nodes + (int64_t)oct * nn);
-  const DevSphereG* __restrict__ geom = sc->sph_geom;
+  // global (address space 1) pointers: through the generic ones loaded from
+  // the scene the walk compiled to flat loads
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(1))) f4v GF4;
+  GF4* __restrict__ nodes_g = (GF4*)(sc->nodes + (int64_t)oct * nn);
+  GF4* __restrict__ geom_g = (GF4*)sc->sph_geom;  // DevSphereG: 2 x 16 B
+  struct {
+    GF4* p;
+    RTP_DEV float4 operator[](int i) const {
+      const f4v v = p[i];
+      return make_float4(v.x, v.y, v.z, v.w);
+    }
+  } nodes{nodes_g};
   auto accept = [&](float t, int orig) {
     if (t < h.t || (t == h.t && h.kind == 1 && orig < h.idx)) {
       h.t = t;
@@ -195,9 +206,9 @@ RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
       if (hit && leaf) {
         const int first = leaf >> 3, cnt = leaf & 7;
         for (int j = first; j < first + cnt; j++) {
-          const float4 g0 = *reinterpret_cast<const float4*>(&geom[j].c[0]);
+          const f4v g0 = geom_g[2 * j], g1 = geom_g[2 * j + 1];  // c, rr | orig
           float t;
-          if (sphere_root(o, d, tmin, mk(g0.x, g0.y, g0.z), g0.w, t)) accept(t, geom[j].orig);
+          if (sphere_root(o, d, tmin, mk(g0.x, g0.y, g0.z), g0.w, t)) accept(t, __float_as_int(g1.x));
         }
       }
       next = (hit && !leaf) ? ni + 1 : skip;

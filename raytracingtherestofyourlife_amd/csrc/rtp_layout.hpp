@@ -73,6 +73,8 @@ struct alignas(16) DevSphereG {
   int32_t pad[3];
 };
 
+static_assert(sizeof(DevSphereG) == 32 && offsetof(DevSphereG, orig) == 16, "spheres_bvh reads DevSphereG as 2 x 16 B");
+
 // Threaded (stackless) BVH node in depth-first order: on a hit of an inner
 // node traversal continues at i+1 (its left child); on a miss, or after a
 // leaf, at `skip` (the first node after this subtree; n_nodes ends the walk).
