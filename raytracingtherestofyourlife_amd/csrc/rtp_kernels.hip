@@ -145,7 +145,7 @@ RTP_DEV bool sphere_root(f3 o, f3 d, float tmin, f3 c, float rr, float& t_out) {
 // only cull (padded on the host; compared with slack here), so no sphere
 // whose root could win is skipped.
 #ifndef RTP_BVH_PREFETCH
-#define RTP_BVH_PREFETCH 1
+#define RTP_BVH_PREFETCH 0  // 1: load node i+1 while testing i (was faster with flat loads; 16% slower with global ones)
 #endif
 RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
   const float tmin = 0.001f;
