@@ -9,14 +9,15 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("nx,ny,world", [(64, 48, 1), (64, 48, 2), (80, 32, 3), (48, 64, 5)])
-def test_gpu_tile_deal_equals_pixel_list(device, nx, ny, world):
+@pytest.mark.parametrize("nx,ny,world,variant", [(64, 48, 1, 0), (64, 48, 2, 0), (80, 32, 3, 0), (48, 64, 5, 0),
+                                                  (64, 48, 3, 3)])
+def test_gpu_tile_deal_equals_pixel_list(device, nx, ny, world, variant):
     import torch
 
     import raytracingtherestofyourlife_amd as rtp
     from raytracingtherestofyourlife_amd import shard
 
-    device.set_cornell_box(0)
+    device.set_cornell_box(variant)  # 3: the 1000-sphere C3 scene (the BVH kernel instance)
     cam = rtp.default_camera()
     s = torch.cuda.current_stream().cuda_stream
     for rank in range(world):
@@ -30,6 +31,7 @@ def test_gpu_tile_deal_equals_pixel_list(device, nx, ny, world):
         torch.cuda.synchronize()
         an, bn = a.cpu().numpy(), b.cpu().numpy()
         assert np.array_equal(an.view(np.uint32), bn.view(np.uint32)), (nx, ny, world, rank)
+    device.set_cornell_box(0)
 
 
 def test_gpu_tile_deal_rejects_partial_tiles(device):
