@@ -52,6 +52,9 @@
 #ifndef RTP_REUSE_CTM
 #define RTP_REUSE_CTM 1  // sphere pdf reuses the light-sphere generator's cos_theta_max
 #endif
+#ifndef RTP_FF_EARLY
+#define RTP_FF_EARLY 1  // pool kernel: first jump-table read overlapped with the radiance loads
+#endif
 #ifndef RTP_FF_MARGIN
 #define RTP_FF_MARGIN 12  // pool kernel: fast-forward when READY holds fewer than idle lanes + this
 #endif
@@ -911,6 +914,13 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
         fseed = s_seed[fslot];
         frem = s_rem[fslot];
       }
+#if RTP_FF_EARLY
+      // the first jump-table read (32 dead depths) is issued before the
+      // radiance loads below, so its latency overlaps theirs
+      uint32_t early = 0;
+      const bool has_early = mine && p.ff[0] != nullptr && (frem & kRemMask) >= 32;
+      if (has_early) early = p.ff[0][fseed];
+#endif
 #if RTP_DEFER_RADIANCE
       if (mine) {
         // back-to-front radiance of the pixel's finished sample (path_radiance),
@@ -923,12 +933,33 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
           const float4* __restrict__ hp = hist_base + fslot;
           const float4 e = hp[(int64_t)k_end * stride];
           float sx = e.x + 0.0f, sy = e.y + 0.0f, sz = e.z + 0.0f;
+#if RTP_FF_EARLY
+          // two history rows per trip, both loads in flight together; the
+          // products stay in the reference's order (depth k_end-1 down to 0)
+          int dd = k_end - 1;
+          for (; dd >= 1; dd -= 2) {
+            const float4 a = hp[(int64_t)dd * stride], b = hp[(int64_t)(dd - 1) * stride];
+            sx = 0.0f + a.x * sx;
+            sy = 0.0f + a.y * sy;
+            sz = 0.0f + a.z * sz;
+            sx = 0.0f + b.x * sx;
+            sy = 0.0f + b.y * sy;
+            sz = 0.0f + b.z * sz;
+          }
+          if (dd == 0) {
+            const float4 a = hp[0];
+            sx = 0.0f + a.x * sx;
+            sy = 0.0f + a.y * sy;
+            sz = 0.0f + a.z * sz;
+          }
+#else
           for (int dd = k_end - 1; dd >= 0; dd--) {
             const float4 a = hp[(int64_t)dd * stride];
             sx = 0.0f + a.x * sx;
             sy = 0.0f + a.y * sy;
             sz = 0.0f + a.z * sz;
           }
+#endif
           c = mk(sx, sy, sz);
         } else {
           const float v = (flags & kEndNonfinite) ? __builtin_nanf("") : 0.0f;
@@ -942,8 +973,14 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
       // jump over 32 / 16 / 8 / 4 dead depths with one table read each
       // (HBM-resident tables of the dead-step map, built once per device),
       // then hash the few remaining depths
+#if RTP_FF_EARLY
+      if (has_early) {
+        fseed = early;
+        frem -= 32;
+      }
+#endif
 #pragma unroll
-      for (int j = 0; j < kFfTables; j++) {
+      for (int j = RTP_FF_EARLY ? 1 : 0; j < kFfTables; j++) {
         const uint32_t* __restrict__ tab = p.ff[j];
         if (tab != nullptr && mine && frem >= (32 >> j)) {
           fseed = tab[fseed];
