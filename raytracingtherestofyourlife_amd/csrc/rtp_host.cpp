@@ -193,6 +193,11 @@ void setup_prefilter(rtp::DevScene* h, const rtp_scene_desc* s, const std::vecto
 // 147.9 / 149.3 ms (3 interleaved rounds each, same box).
 struct FfTables {
   uint32_t* t[rtp::kFfTables] = {};
+  // direct tables: one per remaining-dead-depth count r in [d_first,
+  // d_first + d_count), contiguous (16 GiB each): a finished sample whose r
+  // falls in the range is fast-forwarded by ONE gather instead of a chain
+  uint32_t* direct = nullptr;
+  int d_first = 0, d_count = 0;
   bool tried = false;
   float build_ms = 0.f;
 };
@@ -224,12 +229,47 @@ const FfTables& ff_tables(int device) {
       break;
     }
   }
+  // Direct tables for the counts finished samples most often have.  With
+  // depth 50 a path ending at depth k leaves 49 - k dead depths (50 - k after
+  // a light hit), and paths end early (C2: 3.7 live bounces per sample), so
+  // the default block covers 41..50.  RTP_FF_DIRECT=n (0 disables) and
+  // RTP_FF_DIRECT_FIRST=r choose the block; it shrinks to the free memory.
+  if (T.t[0] != nullptr) {
+    int nd = 10, first = 41;
+    if (const char* env = getenv("RTP_FF_DIRECT")) nd = std::max(0, std::min(32, atoi(env)));
+    if (const char* env = getenv("RTP_FF_DIRECT_FIRST")) first = std::max(1, atoi(env));
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+      const size_t reserve = 8ull << 30;
+      const int fit = free_b > reserve ? (int)((free_b - reserve) / bytes) : 0;
+      nd = std::min(nd, fit);
+    } else {
+      nd = 0;
+    }
+    if (nd > 0 && hipMalloc(&T.direct, bytes * (size_t)nd) == hipSuccess) {
+      bool ok = true;
+      for (int k = 0; k < nd && ok; k++)
+        ok = rtp_launch_build_ff_table(T.direct + (size_t)k * (bytes / 4), first + k, t1, t2, nullptr) == hipSuccess;
+      if (ok) {
+        T.d_first = first;
+        T.d_count = nd;
+      } else {
+        (void)hipFree(T.direct);
+        T.direct = nullptr;
+      }
+    } else {
+      T.direct = nullptr;
+    }
+  }
   (void)hipEventRecord(b, nullptr);
   if (hipEventSynchronize(b) != hipSuccess) {
     for (uint32_t*& p : T.t) {
       if (p) (void)hipFree(p);
       p = nullptr;
     }
+    if (T.direct) (void)hipFree(T.direct);
+    T.direct = nullptr;
+    T.d_count = 0;
   }
   (void)hipEventElapsedTime(&T.build_ms, a, b);
   (void)hipEventDestroy(a);
@@ -772,6 +812,7 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
   if (variant == 2) {
     const FfTables& ft = ff_tables(c->device);
     for (int j = 0; j < rtp::kFfTables; j++) p.ff[j] = ft.t[j];
+    p.ffd = ft.direct, p.ffd_first = ft.d_first, p.ffd_count = ft.d_count;
   }
   if (c->pending) HIP_TRY(hipStreamWaitEvent(stream, c->done, 0));
   HIP_TRY(hipMemsetAsync(c->d_progress, 0, 8, stream));

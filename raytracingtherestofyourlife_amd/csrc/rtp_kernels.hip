@@ -915,11 +915,18 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
         frem = s_rem[fslot];
       }
 #if RTP_FF_EARLY
-      // the first jump-table read (32 dead depths) is issued before the
-      // radiance loads below, so its latency overlaps theirs
+      // the first jump-table read is issued before the radiance loads below,
+      // so its latency overlaps theirs: the direct table of the sample's
+      // remaining count when there is one (then it is the only read), else
+      // the 32-depth table
       uint32_t early = 0;
-      const bool has_early = mine && p.ff[0] != nullptr && (frem & kRemMask) >= 32;
-      if (has_early) early = p.ff[0][fseed];
+      const int frc = frem & kRemMask;
+      const bool has_direct = mine && p.ffd != nullptr && (unsigned)(frc - p.ffd_first) < (unsigned)p.ffd_count;
+      const bool has_early = mine && !has_direct && p.ff[0] != nullptr && frc >= 32;
+      if (has_direct || has_early) {
+        const uint32_t* src = has_direct ? p.ffd + ((uint64_t)(frc - p.ffd_first) << 32) : p.ff[0];
+        early = src[fseed];
+      }
 #endif
 #if RTP_DEFER_RADIANCE
       if (mine) {
@@ -974,7 +981,10 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
       // (HBM-resident tables of the dead-step map, built once per device),
       // then hash the few remaining depths
 #if RTP_FF_EARLY
-      if (has_early) {
+      if (has_direct) {
+        fseed = early;
+        frem = 0;
+      } else if (has_early) {
         fseed = early;
         frem -= 32;
       }

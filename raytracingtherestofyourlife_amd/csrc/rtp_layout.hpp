@@ -170,6 +170,10 @@ struct KParams {
   // RNG jump tables (nullable): ff[j][s] = the state after (32 >> j) dead
   // depths from state s (2^32 entries each, 16 GiB; rtp_host.cpp)
   const uint32_t* ff[kFfTables];
+  // direct tables (nullable): ffd[(r - ffd_first) << 32 | s] = the state after
+  // r dead depths from s, for r in [ffd_first, ffd_first + ffd_count)
+  const uint32_t* ffd;
+  int32_t ffd_first, ffd_count;
 };
 
 // -direct mode (main.cc:120-251): one launch renders the requested AOVs of
