@@ -139,6 +139,20 @@ void setup_prefilter(rtp::DevScene* h, const rtp_scene_desc* s, const std::vecto
     const int flat = 7 & ~(K.m01 | K.m03);
     if (Q.kind < 1 || Q.kind > 6 || (flat != 1 && flat != 2 && flat != 4)) return;
     const int a = flat == 1 ? 0 : flat == 2 ? 1 : 2, b = (a + 1) % 3, c = (a + 2) % 3;
+    if (!Q.para) return;  // (the exact test in plane axes is the parallelogram path)
+    {
+      const int ei = K.m01 == 1 ? 0 : K.m01 == 2 ? 1 : 2, ej = K.m03 == 1 ? 0 : K.m03 == 2 ? 1 : 2;
+      const int ea = 3 - ei - ej;
+      rtp::PreExact& E = h->prex[q];
+      std::memset(&E, 0, sizeof(E));
+      E.i = ei;
+      E.s = (ej == (ei + 1) % 3) ? 1 : -1;
+      E.b = Q.e01[ei], E.c = Q.e03[ej];
+      E.bs = E.s > 0 ? E.b : -E.b, E.cs = E.s > 0 ? E.c : -E.c;
+      E.vi = Q.vv[ei][0], E.va = Q.vv[ea][0], E.vj = Q.vv[ej][0];
+      E.wi = Q.vv[ei][1], E.wa = Q.vv[ea][1], E.wj = Q.vv[ej][1];
+      E.key_lo = Q.key_lo;
+    }
     const int32_t* id = s->quad_points + 4 * kept[Q.orig];
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     const float x = s->points[3 * id[0] + a];

@@ -298,12 +298,14 @@ RTP_DEV void pre_axis(const DevScene* __restrict__ sc, f3 o, f3 d, float ma, flo
   const int b = sc->pre_begin[A], e = sc->pre_begin[A + 1];
   if (b == e) return;
   const float inv = __builtin_amdgcn_rcpf(comp<A>(d));
-  const float oa = comp<A>(o), ob = comp<B>(o), oc = comp<C>(o), db = comp<B>(d), dc = comp<C>(d);
+  const float oa = comp<A>(o);
+  const f2v obc = f2v{comp<B>(o), comp<C>(o)}, dbc = f2v{comp<B>(d), comp<C>(d)};
   for (int i = b; i < e; i++) {
     const PreQuad& P = sc->pre[i];
     const float t = (P.x - oa) * inv;
-    const float ub = fabsf(__builtin_fmaf(t, db, ob) - P.cb) - P.rb;
-    const float uc = fabsf(__builtin_fmaf(t, dc, oc) - P.cc) - P.rc;
+    // the two in-plane coordinates as one packed FMA and one packed subtract
+    const f2v u = __builtin_elementwise_fma(f2v{t, t}, dbc, obc) - f2v{P.cb, P.cc};
+    const float ub = fabsf(u.x) - P.rb, uc = fabsf(u.y) - P.rc;
     const float m = __builtin_fmaf(fabsf(t), ma, mb);
     // t = +-inf (d[A] ~ 0) gives NaN or inf here and at worst a key above
     // every finite one; the exact test rejects such a quad (|det| < eps)
@@ -319,6 +321,44 @@ RTP_DEV void pre_axis(const DevScene* __restrict__ sc, f3 o, f3 d, float ma, flo
 #endif
     k1 = min(k1, key);
   }
+}
+
+// quad_hit_masked<K>'s parallelogram path for an axis-plane quad of any of
+// the kinds 1..6, the kind chosen per lane: the same products, sums and
+// signs (derived in DESIGN.md 4.1), on o and d permuted into the quad's axes.
+#ifndef RTP_PRE_AXIS_EXACT
+#define RTP_PRE_AXIS_EXACT 1
+#endif
+RTP_DEV bool quad_hit_axis(const PreExact& E, f3 o, f3 d, float& t_out) {
+  const bool x0 = E.i == 0, x1 = E.i == 1, pos = E.s > 0;
+  auto perm = [&](f3 v, float& vi, float& va, float& vj) {
+    const float r0 = x0 ? v.x : (x1 ? v.y : v.z);
+    const float r1 = x0 ? v.y : (x1 ? v.z : v.x);
+    const float r2 = x0 ? v.z : (x1 ? v.x : v.y);
+    vi = r0;
+    vj = pos ? r1 : r2;
+    va = pos ? r2 : r1;
+  };
+  float oi, oa, oj, di, da, dj;
+  perm(o, oi, oa, oj);
+  perm(d, di, da, dj);
+  const float Pa = di * E.cs;     // s * d_i c
+  const float Pi = -(da * E.cs);  // -s * d_a c
+  const float det = E.b * Pi;
+  const float inv_det = rcp_det(det);
+  const f2v Ta = f2v{oa, oa} - f2v{E.va, E.wa};
+  const f2v Ti = f2v{oi, oi} - f2v{E.vi, E.wi};
+  const f2v Tj = f2v{oj, oj} - f2v{E.vj, E.wj};
+  const f2v al2 = (Ti * Pi + Ta * Pa) * inv_det;  // (alpha, -ap)
+  const f2v Qj = Ta * E.bs;                       // s * T_a b
+  const f2v Qa = -(Tj * E.bs);                    // -s * T_j b
+  const f2v be2 = (f2v{dj, dj} * Qj + f2v{da, da} * Qa) * inv_det;  // (beta, -bp)
+  const float t = (E.c * Qj.x) * inv_det;
+  const bool ok1 = !(fabsf(det) < kEps) & !(al2.x < 0.0f) & !(be2.x < 0.0f) & !(t < 0.0f);
+  const bool second = (al2.x + be2.x) > 1.0f;
+  const bool bad2 = (al2.y > 0.0f) | (be2.y > 0.0f);
+  t_out = t;
+  return ok1 & !(second & bad2);
 }
 
 template <bool kBvh>
@@ -377,12 +417,19 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
     pre_axis<1>(sc, o, d, ma, mb, k1, k2);
     pre_axis<2>(sc, o, d, ma, mb, k1, k2);
     if (lane_ok && k1 != ~0u) {  // (finite o, d: the generic arithmetic equals the kind's)
+#if RTP_PRE_AXIS_EXACT
+      const auto* gx = (const __attribute__((address_space(1))) PreExact*)(sc->prex);
+      const PreExact& Q = *(const PreExact*)(gx + (k1 & 31u));  // a per-lane (global) load
+      float t;
+      const bool ok = quad_hit_axis(Q, o, d, t);
+#else
       // a per-lane load: measured faster than an LDS copy.  Through a global
       // (address space 1) pointer: the generic one compiled to flat loads.
       const auto* gq = (const __attribute__((address_space(1))) DevQuad*)(sc->quads);
       const DevQuad& Q = *(const DevQuad*)(gq + (k1 & 31u));
       float t;
       const bool ok = quad_hit_masked<0>(Q, o, d, t);
+#endif
       const uint64_t kq = (uint64_t)__float_as_uint(t) << 32 | Q.key_lo;
       key = (ok && t > 0.001f && kq < key) ? kq : key;
     }

@@ -109,11 +109,24 @@ struct alignas(16) DevLights {
 // outward on the host.  Read with uniform (scalar) loads.
 constexpr int kMaxPre = 32;  // prefiltered quads; the key packs the index in 5 bits
 struct alignas(16) PreQuad {
+  float cb, cc;    // centre along axis+1, axis+2 (adjacent: one SGPR pair for packed math)
+  float rb, rc;    // half extents
   float x;         // the plane: coordinate `axis` of every vertex
-  float cb, rb;    // centre / half extent along axis+1
-  float cc, rc;    // centre / half extent along axis+2
   int32_t qpos;    // position in DevScene::quads
   int32_t pad[2];
+};
+
+// The same quads for the prefilter's exact test in the plane's own axes:
+// e01 = b along axis i, e03 = c along axis j, a the third; s = +1 if
+// j == i+1 (mod 3) else -1 (the cross products' sign); the vertex v00 and
+// v11 coordinates permuted to (i, a, j).  Exact parallelograms only.
+struct alignas(16) PreExact {
+  float b, bs, c, cs;  // bs = s*b, cs = s*c
+  float vi, va, vj;    // v00
+  float wi, wa, wj;    // v11
+  int32_t i, s;
+  uint32_t key_lo;     // DevQuad::key_lo
+  int32_t pad[3];
 };
 
 struct alignas(16) DevScene {
@@ -141,6 +154,7 @@ struct alignas(16) DevScene {
   float pre_scale;
   int32_t pad2[2];
   PreQuad pre[kMaxPre];
+  PreExact prex[kMaxPre];  // by quad position (< n_pre)
 };
 
 // camera constants (Camera.cxx:437-474): eye, nlook, delta_x, delta_y
