@@ -110,6 +110,13 @@ void fill_quad(rtp::DevQuad& Q, v3 q, v3 r, v3 s, v3 t) {
     const rtp::QuadKindMasks& K = rtp::kQuadKind[k];
     if (K.m01 == m01 && K.m03 == m03 && K.m21 == m21 && K.m23 == m23) Q.kind = k;
   }
+  // Kinds 1..6 are axis-plane rectangles: their masks force s = (r_I, t_J),
+  // so e23 == -e01 and e21 == -e03 exactly and they are always exact
+  // parallelograms (the prefilter's exact test, quad_hit_axis, relies on
+  // it).  Should one ever fail the check, it is scanned as a general quad
+  // (kind 0: the full products, equal to the masked ones for finite inputs)
+  // and the prefilter stays on for the others.
+  if (Q.kind >= 1 && Q.kind <= 6 && !Q.para) Q.kind = 0;
 }
 
 bool bit_equal(const float* a, const float* b, int n) { return std::memcmp(a, b, sizeof(float) * n) == 0; }
@@ -139,7 +146,7 @@ void setup_prefilter(rtp::DevScene* h, const rtp_scene_desc* s, const std::vecto
     const int flat = 7 & ~(K.m01 | K.m03);
     if (Q.kind < 1 || Q.kind > 6 || (flat != 1 && flat != 2 && flat != 4)) return;
     const int a = flat == 1 ? 0 : flat == 2 ? 1 : 2, b = (a + 1) % 3, c = (a + 2) % 3;
-    if (!Q.para) return;  // (the exact test in plane axes is the parallelogram path)
+    if (!Q.para) return;  // (unreachable: fill_quad moves non-parallelograms to kind 0)
     {
       const int ei = K.m01 == 1 ? 0 : K.m01 == 2 ? 1 : 2, ej = K.m03 == 1 ? 0 : K.m03 == 2 ? 1 : 2;
       const int ea = 3 - ei - ej;

@@ -264,9 +264,11 @@ RTP_DEV void fill_qshade(const DevScene* __restrict__ sc, float* s_qshade) {
 // roundings each of |t*d|, |o| and the vertex coordinates).
 // A quad the exact test accepts (0.001 < t, inside) is therefore a
 // candidate, and t - m is a lower bound of its exact t.  Each lane keeps its
-// two smallest lower bounds, runs the exact test on the first (the generic
-// kind-0 arithmetic on the block's LDS copy of the quad; equal to the kind's own
-// sequence because the skipped terms are exact zeros), and is done when the
+// two smallest lower bounds, runs the exact test on the first (quad_hit_axis
+// on the quad's PreExact record, a per-lane load from the small global prex
+// table: the kind's own parallelogram arithmetic in the quad's axes, bit-equal
+// to it; with RTP_PRE_AXIS_EXACT=0 the generic kind-0 test on its DevQuad,
+// equal because the skipped terms are exact zeros), and is done when the
 // second lower bound exceeds the best exact hit: every other candidate's
 // exact t is larger, so it loses whatever its index.  Otherwise -- near an
 // edge, a near tie, no finite ray, coordinates beyond kPreLim -- the lane
@@ -435,9 +437,9 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
     }
     full = !lane_ok || (k2 & ~31u) <= (uint32_t)(key >> 32);  // k2 = ~0u (none) never is
   }
-  if (full_out) *full_out = pre && full;
+  if (full_out) *full_out = !pre ? 2u : full ? 1u : 0u;  // 2: prefilter off for this scene
 #else
-  if (full_out) *full_out = 0;
+  if (full_out) *full_out = 2u;
 #endif
   if (__ballot(full)) {
     if (full) {

@@ -104,8 +104,11 @@ def test_gpu_prefilter_equals_exact_scan(device, variant):
     got = device.debug_closest_hit(rays)
     bad = np.nonzero((got[:, 0:3] != got[:, 3:6]).any(1))[0]
     assert bad.size == 0, f"{bad.size} rays differ, first {rays[bad[:3]].tolist()} -> {got[bad[:3]].tolist()}"
-    # the prefilter must actually engage on this scene (axis-plane quads)
-    assert got[:, 6].mean() < 0.5
+    # the prefilter must actually engage on this scene (axis-plane quads):
+    # column 6 is 0 (prefilter decided), 1 (fell back to the exact scan) or
+    # 2 (prefilter off for the scene)
+    assert (got[:, 6] != 2).all()
+    assert (got[:, 6] == 1).mean() < 0.5
 
 
 def test_gpu_prefilter_fallback_rate(device):
@@ -117,7 +120,8 @@ def test_gpu_prefilter_fallback_rate(device):
     ordinary = np.concatenate([rays[6 * k:], rays[k:2 * k]])
     got = device.debug_closest_hit(ordinary)
     assert (got[:, 0:3] == got[:, 3:6]).all()
-    assert got[:, 6].mean() < 0.01, got[:, 6].mean()
+    assert (got[:, 6] != 2).all()
+    assert (got[:, 6] == 1).mean() < 0.01, (got[:, 6] == 1).mean()
 
 
 def test_gpu_prefilter_bvh_scene_equals_exact(device):
@@ -129,3 +133,34 @@ def test_gpu_prefilter_bvh_scene_equals_exact(device):
     got = device.debug_closest_hit(rays)
     assert (got[:, 0:3] == got[:, 3:6]).all()
     device.set_cornell_box(0)
+
+
+def test_gpu_prefilter_with_trapezoid_in_axis_plane(device):
+    """A scene whose axis-plane quads include a non-parallelogram (a
+    trapezoid in the plane z = const, scanned as a general quad): the
+    prefilter stays on for the other axis-plane quads and every hit equals
+    the exact scan's."""
+    import raytracingtherestofyourlife_amd as rtp
+
+    cb = rtp.CornellBox(0)
+    ds = cb.buildDataSet()
+    P = np.asarray(ds.coords, dtype=np.float32).reshape(-1, 3).copy()
+    Q = np.asarray(ds.cellset.quad_points).reshape(-1, 4).copy()
+    # quad 12 lies in a z-plane (e01 along x, e03 along y): move its v11
+    # along x within the plane, so e21 gains an x component (a trapezoid)
+    v11 = int(Q[12, 2])
+    P = np.concatenate([P, P[v11:v11 + 1]], 0)
+    P[-1, 0] += np.float32(0.05)
+    Q[12, 2] = len(P) - 1
+    device.set_scene(P, Q, cb.matIdx[0], cb.texIdx[0], ds.cellset.sphere_points, cb.SphereRadii, cb.matIdx[1],
+                     cb.texIdx[1], cb.matType, cb.texType, cb.tex, cb.light_quad_points, cb.light_sphere_point,
+                     cb.ior)
+    try:
+        verts = P[Q]
+        rays = stress_rays(verts, 1 << 20, 12)
+        got = device.debug_closest_hit(rays)
+        bad = np.nonzero((got[:, 0:3] != got[:, 3:6]).any(1))[0]
+        assert bad.size == 0, f"{bad.size} rays differ, first {rays[bad[:3]].tolist()}"
+        assert (got[:, 6] != 2).all(), "prefilter switched off by one non-parallelogram quad"
+    finally:
+        device.set_cornell_box(0)

@@ -20,6 +20,6 @@ k = len(rays) // 8
 names = ["edge-aimed", "from surfaces", "grazing", "on planes/axis", "unnormalised", "out of range", "camera",
          "to light"]
 for i, n in enumerate(names):
-    p = got[i * k:(i + 1) * k, 6].mean()
+    p = (got[i * k:(i + 1) * k, 6] == 1).mean()
     print(f"{n:16s} fallback {p:.5f}  waves {1 - (1 - p) ** 57:.3f}  mismatches "
           f"{int((got[i * k:(i + 1) * k, 0:3] != got[i * k:(i + 1) * k, 3:6]).any(1).sum())}")
