@@ -326,8 +326,11 @@ RTP_DEV f2v dot_m2l(const float* x, const f2v (&y)[3]) {  // dot_m with a shared
   else return f2v{0.0f, 0.0f};
 }
 
-template <int K>
-RTP_DEV bool quad_hit_masked(const DevQuad& Q, f3 o, f3 d, float& t_out) {
+// G: the quad's scan head (a DevQuad, or a QuadGeom copy already in
+// registers); M: the quad in memory, read only for the second triangle's
+// edges of a quad that is not an exact parallelogram.
+template <int K, class G = DevQuad>
+RTP_DEV bool quad_hit_masked(const G& Q, const DevQuad& M, f3 o, f3 d, float& t_out) {
   constexpr int M01 = kQuadKind[K].m01, M03 = kQuadKind[K].m03, M21 = kQuadKind[K].m21, M23 = kQuadKind[K].m23;
   constexpr int MP = cross_mask(M03), MQ = cross_mask(M01), MPp = cross_mask(M21), MQp = cross_mask(M23);
   const float dv[3] = {d.x, d.y, d.z};
@@ -377,12 +380,12 @@ RTP_DEV bool quad_hit_masked(const DevQuad& Q, f3 o, f3 d, float& t_out) {
   const float t = dot_m<M03 & MQ>(Q.e03, Qv) * inv_det;
   bool ok = !(fabsf(det) < kEps) && !(alpha < 0.0f) && !(beta < 0.0f) && !(t < 0.0f);
   if (ok && (alpha + beta) > 1.0f) {
-    const float Pp[3] = {cross_c<M21, 0>(dv, Q.e21), cross_c<M21, 1>(dv, Q.e21), cross_c<M21, 2>(dv, Q.e21)};
-    const float detp = dot_m<M23 & MPp>(Q.e23, Pp);
+    const float Pp[3] = {cross_c<M21, 0>(dv, M.e21), cross_c<M21, 1>(dv, M.e21), cross_c<M21, 2>(dv, M.e21)};
+    const float detp = dot_m<M23 & MPp>(M.e23, Pp);
     const float inv_detp = rcp_det(detp);
     const float Tp[3] = {o.x - Q.vv[0][1], o.y - Q.vv[1][1], o.z - Q.vv[2][1]};
     const float ap = dot_m<MPp>(Tp, Pp) * inv_detp;
-    const float Qp[3] = {cross_c<M23, 0>(Tp, Q.e23), cross_c<M23, 1>(Tp, Q.e23), cross_c<M23, 2>(Tp, Q.e23)};
+    const float Qp[3] = {cross_c<M23, 0>(Tp, M.e23), cross_c<M23, 1>(Tp, M.e23), cross_c<M23, 2>(Tp, M.e23)};
     const float bp = dot_m<MQp>(dv, Qp) * inv_detp;
     ok = !(fabsf(detp) < kEps) && !(ap < 0.0f) && !(bp < 0.0f);
   }
@@ -393,17 +396,17 @@ RTP_DEV bool quad_hit_masked(const DevQuad& Q, f3 o, f3 d, float& t_out) {
 // Q.kind is wave-uniform (every lane tests the same quad): scalar branch.
 RTP_DEV bool quad_hit(const DevQuad& Q, f3 o, f3 d, float& t_out) {
   switch (Q.kind) {
-    case 1: return quad_hit_masked<1>(Q, o, d, t_out);
-    case 2: return quad_hit_masked<2>(Q, o, d, t_out);
-    case 3: return quad_hit_masked<3>(Q, o, d, t_out);
-    case 4: return quad_hit_masked<4>(Q, o, d, t_out);
-    case 5: return quad_hit_masked<5>(Q, o, d, t_out);
-    case 6: return quad_hit_masked<6>(Q, o, d, t_out);
-    case 7: return quad_hit_masked<7>(Q, o, d, t_out);
-    case 8: return quad_hit_masked<8>(Q, o, d, t_out);
-    case 9: return quad_hit_masked<9>(Q, o, d, t_out);
-    case 10: return quad_hit_masked<10>(Q, o, d, t_out);
-    default: return quad_hit_masked<0>(Q, o, d, t_out);
+    case 1: return quad_hit_masked<1>(Q, Q, o, d, t_out);
+    case 2: return quad_hit_masked<2>(Q, Q, o, d, t_out);
+    case 3: return quad_hit_masked<3>(Q, Q, o, d, t_out);
+    case 4: return quad_hit_masked<4>(Q, Q, o, d, t_out);
+    case 5: return quad_hit_masked<5>(Q, Q, o, d, t_out);
+    case 6: return quad_hit_masked<6>(Q, Q, o, d, t_out);
+    case 7: return quad_hit_masked<7>(Q, Q, o, d, t_out);
+    case 8: return quad_hit_masked<8>(Q, Q, o, d, t_out);
+    case 9: return quad_hit_masked<9>(Q, Q, o, d, t_out);
+    case 10: return quad_hit_masked<10>(Q, Q, o, d, t_out);
+    default: return quad_hit_masked<0>(Q, Q, o, d, t_out);
   }
 }
 

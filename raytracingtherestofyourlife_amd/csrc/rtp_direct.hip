@@ -34,7 +34,7 @@ RTP_DEV void scan_direct(const DevScene* __restrict__ sc, int g, f3 o, f3 d, uin
   for (int q = b; q < e; q++) {
     const DevQuad& Q = sc->quads[q];
     float t;
-    const bool ok = quad_hit_masked<K>(Q, o, d, t);
+    const bool ok = quad_hit_masked<K>(Q, Q, o, d, t);
     const uint64_t key = (uint64_t)__float_as_uint(t) << 32 | Q.key_lo;
     best = (ok && t > 0.0f && key < best) ? key : best;
   }

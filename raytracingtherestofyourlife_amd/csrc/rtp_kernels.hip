@@ -98,9 +98,35 @@ RTP_DEV void scan_kind(const DevScene* __restrict__ sc, int g, f3 o, f3 d, uint6
   for (int q = b; q < e; q++) {
     const DevQuad& Q = sc->quads[q];
     float t;
-    const bool ok = quad_hit_masked<K>(Q, o, d, t);
+    const bool ok = quad_hit_masked<K>(Q, Q, o, d, t);
     const uint64_t key = (uint64_t)__float_as_uint(t) << 32 | Q.key_lo;
     best = (ok && t > 0.001f && key < best) ? key : best;
+  }
+}
+// The same scan with the quads' 64-byte scan heads (QuadGeom) fetched as one
+// s_load_dwordx16 each, the NEXT quad's issued before the current one is
+// tested, so its scalar-load latency hides behind the test's VALU work (the
+// field-by-field loads compiled to ~5 dependent s_load / s_waitcnt round
+// trips per quad).  `cur` holds quad b's head on entry and quad e's (the next
+// group's first: the groups are contiguous in scan order) on exit.
+#ifndef RTP_SCAN_PF
+#define RTP_SCAN_PF 1
+#endif
+typedef uint32_t u16v __attribute__((ext_vector_type(16)));
+RTP_DEV u16v quad_head(const DevScene* __restrict__ sc, int q) {
+  return reinterpret_cast<const u16v*>(sc->quads)[2 * min(q, kMaxQuads - 1)];
+}
+template <int K>
+RTP_DEV void scan_kind_pf(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d, uint64_t& best, u16v& cur) {
+  for (int q = b; q < e; q++) {
+    const u16v nxt = quad_head(sc, q + 1);
+    QuadGeom G;
+    __builtin_memcpy(&G, &cur, sizeof(G));
+    float t;
+    const bool ok = quad_hit_masked<K>(G, sc->quads[q], o, d, t);
+    const uint64_t key = (uint64_t)__float_as_uint(t) << 32 | G.key_lo;
+    best = (ok && t > 0.001f && key < best) ? key : best;
+    cur = nxt;
   }
 }
 #else
@@ -110,7 +136,7 @@ RTP_DEV void scan_kind(const DevScene* __restrict__ sc, int g, f3 o, f3 d, Hit& 
   for (int q = b; q < e; q++) {
     const DevQuad& Q = sc->quads[q];
     float t;
-    const bool ok = quad_hit_masked<K>(Q, o, d, t);
+    const bool ok = quad_hit_masked<K>(Q, Q, o, d, t);
     const int orig = Q.orig;
     if (ok && t > 0.001f && (t < h.t || (t == h.t && orig < best))) {
       h.t = t;
@@ -294,16 +320,32 @@ RTP_DEV float comp(f3 v) {
 // k1 <= k2: the two smallest candidate keys {bits(t - m) & ~31, quad position}
 // (positive floats order like their bit patterns; rounding the low bits
 // down keeps the lower bound).  No candidate: ~0u.
+// RTP_PRE_PF: each PreQuad as one s_load_dwordx8, the next one's issued
+// before the current one is tested (as scan_kind_pf); `cur` carries quad b's
+// record in and quad e's (the next axis group's first) out.
+#ifndef RTP_PRE_PF
+#define RTP_PRE_PF 1
+#endif
+typedef uint32_t u8v __attribute__((ext_vector_type(8)));
+RTP_DEV u8v pre_rec(const DevScene* __restrict__ sc, int i) {
+  return reinterpret_cast<const u8v*>(sc->pre)[min(i, kMaxPre - 1)];
+}
 template <int A>
-RTP_DEV void pre_axis(const DevScene* __restrict__ sc, f3 o, f3 d, float ma, float mb, uint32_t& k1, uint32_t& k2) {
+RTP_DEV void pre_axis(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d, float ma, float mb, uint32_t& k1,
+                      uint32_t& k2, u8v& cur) {
   constexpr int B = (A + 1) % 3, C = (A + 2) % 3;
-  const int b = sc->pre_begin[A], e = sc->pre_begin[A + 1];
   if (b == e) return;
   const float inv = __builtin_amdgcn_rcpf(comp<A>(d));
   const float oa = comp<A>(o);
   const f2v obc = f2v{comp<B>(o), comp<C>(o)}, dbc = f2v{comp<B>(d), comp<C>(d)};
   for (int i = b; i < e; i++) {
+#if RTP_PRE_PF
+    const u8v nxt = pre_rec(sc, i + 1);
+    PreQuad P;
+    __builtin_memcpy(&P, &cur, sizeof(P));
+#else
     const PreQuad& P = sc->pre[i];
+#endif
     const float t = (P.x - oa) * inv;
     // the two in-plane coordinates as one packed FMA and one packed subtract
     const f2v u = __builtin_elementwise_fma(f2v{t, t}, dbc, obc) - f2v{P.cb, P.cc};
@@ -322,6 +364,9 @@ RTP_DEV void pre_axis(const DevScene* __restrict__ sc, f3 o, f3 d, float ma, flo
     k2 = min(k2, max(k1, key));
 #endif
     k1 = min(k1, key);
+#if RTP_PRE_PF
+    cur = nxt;
+#endif
   }
 }
 
@@ -330,6 +375,12 @@ RTP_DEV void pre_axis(const DevScene* __restrict__ sc, f3 o, f3 d, float ma, flo
 // signs (derived in DESIGN.md 4.1), on o and d permuted into the quad's axes.
 #ifndef RTP_PRE_AXIS_EXACT
 #define RTP_PRE_AXIS_EXACT 1
+#endif
+#ifndef RTP_PREX_WIDE
+#define RTP_PREX_WIDE 1  // the candidate's PreExact as four 16-byte loads issued together
+#endif
+#ifndef RTP_PREX_EARLY
+#define RTP_PREX_EARLY 0  // 1: ... issued before the exact scan of kinds 7..10, 0 (which hides their latency)
 #endif
 RTP_DEV bool quad_hit_axis(const PreExact& E, f3 o, f3 d, float& t_out) {
   const bool x0 = E.i == 0, x1 = E.i == 1, pos = E.s > 0;
@@ -399,14 +450,30 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
 #if RTP_HIT_KEY
   uint64_t key = kNoHitKey;
   // kinds 7..10 and 0: the exact scan, always (their keys are final)
-  scan_kind<7>(sc, 6, o, d, key);
-  scan_kind<8>(sc, 7, o, d, key);
-  scan_kind<9>(sc, 8, o, d, key);
-  scan_kind<10>(sc, 9, o, d, key);
-  scan_kind<0>(sc, 10, o, d, key);
+  auto scan_rest = [&]() {
+#if RTP_SCAN_PF
+    const int g6 = sc->kind_begin[6], g7 = sc->kind_begin[7], g8 = sc->kind_begin[8], g9 = sc->kind_begin[9],
+              g10 = sc->kind_begin[10], g11 = sc->kind_begin[11];
+    u16v cur = quad_head(sc, g6);
+    scan_kind_pf<7>(sc, g6, g7, o, d, key, cur);
+    scan_kind_pf<8>(sc, g7, g8, o, d, key, cur);
+    scan_kind_pf<9>(sc, g8, g9, o, d, key, cur);
+    scan_kind_pf<10>(sc, g9, g10, o, d, key, cur);
+    scan_kind_pf<0>(sc, g10, g11, o, d, key, cur);
+#else
+    scan_kind<7>(sc, 6, o, d, key);
+    scan_kind<8>(sc, 7, o, d, key);
+    scan_kind<9>(sc, 8, o, d, key);
+    scan_kind<10>(sc, 9, o, d, key);
+    scan_kind<0>(sc, 10, o, d, key);
+#endif
+  };
   bool full = true;  // this lane needs the exact scan of the axis-plane quads (kinds 1..6)
 #if RTP_PREFILTER
   const bool pre = prefilter && sc->n_pre > 0;  // wave-uniform
+#if !RTP_PREX_EARLY
+  scan_rest();
+#endif
   if (pre) {
     const bool lane_ok = (int)(fabsf(o.x) <= kPreLimD) & (int)(fabsf(o.y) <= kPreLimD) &
                          (int)(fabsf(o.z) <= kPreLimD) & (int)(fabsf(d.x) <= kPreLimD) &
@@ -415,9 +482,33 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
     const float omax = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
     const float ma = kPreK * dmax, mb = kPreK * (omax + (sc->pre_scale + 1.0f));
     uint32_t k1 = ~0u, k2 = ~0u;
-    pre_axis<0>(sc, o, d, ma, mb, k1, k2);
-    pre_axis<1>(sc, o, d, ma, mb, k1, k2);
-    pre_axis<2>(sc, o, d, ma, mb, k1, k2);
+    const int p0 = sc->pre_begin[0], p1 = sc->pre_begin[1], p2 = sc->pre_begin[2], p3 = sc->pre_begin[3];
+    u8v pcur = RTP_PRE_PF ? pre_rec(sc, p0) : u8v{};
+    pre_axis<0>(sc, p0, p1, o, d, ma, mb, k1, k2, pcur);
+    pre_axis<1>(sc, p1, p2, o, d, ma, mb, k1, k2, pcur);
+    pre_axis<2>(sc, p2, p3, o, d, ma, mb, k1, k2, pcur);
+#if RTP_PRE_AXIS_EXACT && RTP_PREX_WIDE
+    // the candidate's PreExact record: four 16-byte per-lane loads issued
+    // together (every lane: k1 = ~0u reads record 31, in bounds, unused),
+    // with RTP_PREX_EARLY before the exact scan of kinds 7..10 and 0, whose
+    // VALU work then hides their latency (field-wise they compiled to ~4
+    // dependent load / s_waitcnt vmcnt round trips)
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const auto* gx = (const __attribute__((address_space(1))) f4v*)(sc->prex) + 4 * (k1 & 31u);
+    f4v xr[4] = {gx[0], gx[1], gx[2], gx[3]};
+    static_assert(sizeof(PreExact) == sizeof(xr), "PreExact is four 16-byte loads");
+#if RTP_PREX_EARLY
+    scan_rest();
+#endif
+    if (lane_ok && k1 != ~0u) {  // (finite o, d: the generic arithmetic equals the kind's)
+      PreExact Q;
+      __builtin_memcpy(&Q, xr, sizeof(Q));
+      float t;
+      const bool ok = quad_hit_axis(Q, o, d, t);
+#else
+#if RTP_PREX_EARLY
+    scan_rest();
+#endif
     if (lane_ok && k1 != ~0u) {  // (finite o, d: the generic arithmetic equals the kind's)
 #if RTP_PRE_AXIS_EXACT
       const auto* gx = (const __attribute__((address_space(1))) PreExact*)(sc->prex);
@@ -430,25 +521,44 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
       const auto* gq = (const __attribute__((address_space(1))) DevQuad*)(sc->quads);
       const DevQuad& Q = *(const DevQuad*)(gq + (k1 & 31u));
       float t;
-      const bool ok = quad_hit_masked<0>(Q, o, d, t);
+      const bool ok = quad_hit_masked<0>(Q, Q, o, d, t);
+#endif
 #endif
       const uint64_t kq = (uint64_t)__float_as_uint(t) << 32 | Q.key_lo;
       key = (ok && t > 0.001f && kq < key) ? kq : key;
     }
     full = !lane_ok || (k2 & ~31u) <= (uint32_t)(key >> 32);  // k2 = ~0u (none) never is
   }
+#if RTP_PREX_EARLY
+  else {
+    scan_rest();
+  }
+#endif
   if (full_out) *full_out = !pre ? 2u : full ? 1u : 0u;  // 2: prefilter off for this scene
 #else
+  scan_rest();
   if (full_out) *full_out = 2u;
 #endif
   if (__ballot(full)) {
     if (full) {
+#if RTP_SCAN_PF
+      const int g0 = sc->kind_begin[0], g1 = sc->kind_begin[1], g2 = sc->kind_begin[2], g3 = sc->kind_begin[3],
+                g4 = sc->kind_begin[4], g5 = sc->kind_begin[5], g6 = sc->kind_begin[6];
+      u16v cur = quad_head(sc, g0);
+      scan_kind_pf<1>(sc, g0, g1, o, d, key, cur);
+      scan_kind_pf<2>(sc, g1, g2, o, d, key, cur);
+      scan_kind_pf<3>(sc, g2, g3, o, d, key, cur);
+      scan_kind_pf<4>(sc, g3, g4, o, d, key, cur);
+      scan_kind_pf<5>(sc, g4, g5, o, d, key, cur);
+      scan_kind_pf<6>(sc, g5, g6, o, d, key, cur);
+#else
       scan_kind<1>(sc, 0, o, d, key);
       scan_kind<2>(sc, 1, o, d, key);
       scan_kind<3>(sc, 2, o, d, key);
       scan_kind<4>(sc, 3, o, d, key);
       scan_kind<5>(sc, 4, o, d, key);
       scan_kind<6>(sc, 5, o, d, key);
+#endif
     }
   }
   (void)best;

@@ -41,20 +41,38 @@ constexpr QuadKindMasks kQuadKind[kQuadKinds] = {
     {7, 7, 5, 5}};  // 10: the small box's top (CornellBox.cpp's y=333 vertex): only e21/e23 are flat
 
 // One quad of the Lagae-Dutre test (Surface.h:31-161) with v00=q, v10=r,
-// v11=s, v01=t.  Read with uniform (scalar) loads.
+// v11=s, v01=t.  Read with uniform (scalar) loads.  The first 64 bytes are
+// everything the closest-hit scan of an exact parallelogram reads (QuadGeom):
+// the scan fetches them as one s_load_dwordx16, the next quad's while it
+// tests the current one.
 struct alignas(16) DevQuad {
   float vv[3][2];                // (v00[k], v11[k]) interleaved: one SGPR pair per axis for packed math
   float e01[3], e03[3];          // e01 = v10-v00, e03 = v01-v00
+  uint32_t key_lo;               // orig << 8 | scan position: low word of the (t, orig) hit key
+  int32_t para;                  // e23 == -e01 and e21 == -e03 bit for bit (exact parallelogram)
+  int32_t orig;                  // index in the reference's quad order (tie-break of equal t)
+  int32_t kind;                  // index into kQuadKind
   float e21[3], e23[3];          // e21 = v10-v11, e23 = v01-v11
   float n[3];                    // Normalize(TriangleNormal(q,r,s)), unflipped
   float alb[3];                  // tex[texType[texIdx]]
   int32_t mt;                    // matType[matIdx]
-  int32_t kind;                  // index into kQuadKind
-  int32_t orig;                  // index in the reference's quad order (tie-break of equal t)
-  int32_t para;                  // e23 == -e01 and e21 == -e03 bit for bit (exact parallelogram)
-  uint32_t key_lo;               // orig << 8 | scan position: low word of the (t, orig) hit key
   int32_t pad[3];
 };
+// The scan-time head of a DevQuad (same field offsets).
+struct alignas(16) QuadGeom {
+  float vv[3][2];
+  float e01[3], e03[3];
+  uint32_t key_lo;
+  int32_t para;
+  int32_t orig;
+  int32_t kind;
+};
+static_assert(sizeof(DevQuad) == 128 && sizeof(QuadGeom) == 64 && offsetof(DevQuad, e21) == 64,
+              "DevQuad: 64-byte scan head + 64-byte tail");
+static_assert(offsetof(DevQuad, key_lo) == offsetof(QuadGeom, key_lo) &&
+                  offsetof(DevQuad, para) == offsetof(QuadGeom, para) &&
+                  offsetof(DevQuad, e03) == offsetof(QuadGeom, e03),
+              "QuadGeom mirrors the head of DevQuad");
 
 struct alignas(16) DevSphere {
   float c[3];
@@ -115,6 +133,7 @@ struct alignas(16) PreQuad {
   int32_t qpos;    // position in DevScene::quads
   int32_t pad[2];
 };
+static_assert(sizeof(PreQuad) == 32, "the prefilter scan reads a PreQuad as one s_load_dwordx8");
 
 // The same quads for the prefilter's exact test in the plane's own axes:
 // e01 = b along axis i, e03 = c along axis j, a the third; s = +1 if

@@ -7,7 +7,7 @@ how often a block runs is not known here, but the per-region totals of the
 straight-line parts of a bounce (quad tests, generator, pdfs) are the VALU
 instructions one bounce step issues there.
 
-usage: python tools/isa_attrib.py [--kernel SUBSTR] [--defines -DX=1 ...] [--top N] [--blocks]
+usage: python tools/isa_attrib.py [--kernel SUBSTR] [--defines="-DX=1 ..."] [--top N] [--blocks]
 """
 from __future__ import annotations
 
@@ -44,14 +44,14 @@ def kernel_lines(asm: str, substr: str) -> list[str]:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--kernel", default="rtp_render_poolILb0ELb0ELb1E")
-    ap.add_argument("--defines", nargs="*", default=[])
+    ap.add_argument("--defines", default="", help='e.g. --defines="-DRTP_X=0 -DRTP_Y=1"')
     ap.add_argument("--asm", default="/tmp/rtp_isa.s")
     ap.add_argument("--no-compile", action="store_true")
     ap.add_argument("--top", type=int, default=60)
     ap.add_argument("--blocks", action="store_true")
     a = ap.parse_args()
     if not a.no_compile:
-        compile_asm(a.asm, a.defines)
+        compile_asm(a.asm, a.defines.split())
     body, files = kernel_lines(a.asm, a.kernel)
     loc = ("?", 0)
     per_line = collections.Counter()
