@@ -26,6 +26,7 @@ struct f3 {
 };
 RTP_DEV f3 mk(float x, float y, float z) { return f3{x, y, z}; }
 RTP_DEV f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
+RTP_DEV f3 ld3(const __attribute__((address_space(4))) float* p) { return f3{p[0], p[1], p[2]}; }  // kernarg / constant
 RTP_DEV f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
 RTP_DEV f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
 RTP_DEV f3 scl(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }

@@ -810,6 +810,8 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
                   uint32_t seed_base, int64_t pixel_begin, int64_t npix, const int64_t* d_ids, float* d_out,
                   uint32_t* d_seed, uint32_t* d_live, hipStream_t stream, double* kernel_ms,
                   const int32_t* tile = nullptr) {
+  // the kernels index a launch's entries with 32-bit integers
+  if (npix > INT32_MAX) return fail(RTP_ERR_INVALID_ARGUMENT, "render: more than 2^31-1 pixels in one launch");
   HIP_TRY(hipSetDevice(c->device));
   rtp::KParams p{};
   if (tile) p.tile_tx = tile[0], p.tile_world = tile[1], p.tile_rank = tile[2];

@@ -64,6 +64,9 @@
 #ifndef RTP_CRIT_FF
 #define RTP_CRIT_FF 100  // pool kernel: lag (per mille of the wave's average samples) that makes a pixel critical
 #endif
+#ifndef RTP_CAM_RELOAD
+#define RTP_CAM_RELOAD 1  // pool kernel: refill reads the camera from the kernel arguments, not from spilled SGPRs
+#endif
 #ifndef RTP_MERGED_GEN
 #define RTP_MERGED_GEN 1  // branch-free generator pass (bounce); 0: the three divergent branches
 #endif
@@ -599,7 +602,8 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
 }
 
 // Camera::RayGen (Camera.cxx:482-524): 2 draws, jittered direction
-RTP_DEV f3 camera_ray(const DevCamera& cam, int pi, int pj, int nx, int ny, uint32_t& seed) {
+template <class Cam>  // DevCamera, or one read through an address-space-4 (kernarg) reference
+RTP_DEV f3 camera_ray(const Cam& cam, int pi, int pj, int nx, int ny, uint32_t& seed) {
   float ru = randf(seed);
   float rv = randf(seed);
   f3 rd = add(add(ld3(cam.nlook), scl(ld3(cam.dx), ((2.f * ((float)pi + (1.f - ru)) - (float)nx) / 2.0f))),
@@ -848,8 +852,9 @@ RTP_DEV f3 path_radiance(int result, int k, f3 emit, bool nonfinite, const float
 
 // Tile-deal index arithmetic: q = ti / tx from a float reciprocal, then one
 // correction each way (ti < 2^24, so the estimate is off by at most one).
-RTP_DEV int64_t tile_pixel(const KParams& p, int64_t k) {
-  const int ti = (int)(k >> 8) * p.tile_world + p.tile_rank, within = (int)(k & 255);
+template <class KP>
+RTP_DEV int64_t tile_pixel(const KP& p, int k) {
+  const int ti = (k >> 8) * p.tile_world + p.tile_rank, within = k & 255;
   int ty = (int)((float)ti * __builtin_amdgcn_rcpf((float)p.tile_tx));
   ty += (ty + 1) * p.tile_tx <= ti;
   ty -= ty * p.tile_tx > ti;
@@ -859,8 +864,8 @@ RTP_DEV int64_t tile_pixel(const KParams& p, int64_t k) {
 // kTiles: a separate kernel instance (rtp_render_tiles_device).  A runtime
 // branch here changed the compiler's code for the whole scheduling loop of
 // the other modes (+9% time), as other additions to the refill path did.
-template <bool kTiles = false>
-RTP_DEV int64_t pixel_of(const KParams& p, int64_t k) {
+template <bool kTiles = false, class KP>
+RTP_DEV int64_t pixel_of(const KP& p, int k) {  // k < npix <= INT32_MAX (launch() checks)
   if constexpr (kTiles) return tile_pixel(p, k);
   else return p.pixel_ids ? p.pixel_ids[k] : p.pixel_begin + k;
 }
@@ -968,6 +973,10 @@ RTP_DEV void set_priority(float lag) {  // s_setprio needs an immediate
 #ifndef RTP_POOL_MAX_VGPR
 #define RTP_POOL_MAX_VGPR 96
 #endif
+// byte offset of the KParams argument in rtp_render_pool's kernarg segment
+// (after the 8-byte scene pointer; checked against the code object's
+// argument metadata by tests/test_abi.py)
+constexpr int kKParamsOffset = 8;
 template <bool kStats, bool kBvh, bool kTiles = false>
 #if RTP_POOL_MAX_VGPR > 0
 #define RTP_POOL_VGPR_ATTR __attribute__((amdgpu_num_vgpr(RTP_POOL_MAX_VGPR)))
@@ -1217,9 +1226,22 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
 #if RTP_DEFER_RADIANCE
         hist = hist_base + slot;
 #endif
-        const int64_t pix = pixel_of<kTiles>(p, (int64_t)slot * n_waves + w);
-        const int pi = (int32_t)pix % p.nx, pj = (int32_t)pix / p.nx;
-        ps.dir = camera_ray(p.cam, pi, pj, p.nx, p.ny, seed);
+#if RTP_CAM_RELOAD
+        // the camera and tile constants re-read from the kernel arguments
+        // here (scalar loads): kept live through the loop they were SGPRs
+        // spilled to VGPR lanes, ~30 v_readlane per refill
+        // (through the kernarg segment pointer: &p would copy p to scratch)
+        typedef const __attribute__((address_space(4))) KParams CKP;
+        CKP* pp = (CKP*)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() +
+                         kKParamsOffset);
+        asm volatile("" : "+s"(pp));
+        CKP& P = *pp;
+#else
+        const KParams& P = p;
+#endif
+        const int64_t pix = pixel_of<kTiles>(P, slot * n_waves + w);  // (32-bit: a 64-bit index spilled)
+        const int pi = (int32_t)pix % P.nx, pj = (int32_t)pix / P.nx;
+        ps.dir = camera_ray(P.cam, pi, pj, P.nx, P.ny, seed);
 #if RTP_DUP == 7
         {
           uint32_t s2 = seed;
@@ -1228,7 +1250,7 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
           RTP_SINK(d2.x, seed);
         }
 #endif
-        ps.org = eye;
+        ps.org = RTP_CAM_RELOAD ? ld3(P.cam.eye) : eye;
         ps.d = 0;
         ps.nonfinite = false;
         has_path = true;
