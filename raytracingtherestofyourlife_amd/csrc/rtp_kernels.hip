@@ -55,6 +55,9 @@
 #ifndef RTP_FF_EARLY
 #define RTP_FF_EARLY 1  // pool kernel: first jump-table read overlapped with the radiance loads
 #endif
+#ifndef RTP_FF_FALL
+#define RTP_FF_FALL 0  // pool kernel: a fast-forward batch is followed by refill + bounce in the same iteration
+#endif
 #ifndef RTP_FF_MARGIN
 #define RTP_FF_MARGIN 12  // pool kernel: fast-forward when READY holds fewer than idle lanes + this
 #endif
@@ -72,6 +75,8 @@
 #endif
 
 namespace rtp {
+
+typedef uint32_t u16v __attribute__((ext_vector_type(16)));  // 64 bytes: one s_load_dwordx16
 
 struct Hit {
   float t;
@@ -115,12 +120,36 @@ RTP_DEV void scan_kind(const DevScene* __restrict__ sc, int g, f3 o, f3 d, uint6
 #ifndef RTP_SCAN_PF
 #define RTP_SCAN_PF 1
 #endif
-typedef uint32_t u16v __attribute__((ext_vector_type(16)));
 RTP_DEV u16v quad_head(const DevScene* __restrict__ sc, int q) {
   return reinterpret_cast<const u16v*>(sc->quads)[2 * min(q, kMaxQuads - 1)];
 }
+#ifndef RTP_SCAN_PP
+#define RTP_SCAN_PP 0  // ping-pong the two head registers (no copy of the prefetched head per quad)
+#endif
+template <int K>
+RTP_DEV void scan_one(const DevScene* __restrict__ sc, int q, const u16v& head, f3 o, f3 d, uint64_t& best) {
+  QuadGeom G;
+  __builtin_memcpy(&G, &head, sizeof(G));
+  float t;
+  const bool ok = quad_hit_masked<K>(G, sc->quads[q], o, d, t);
+  const uint64_t key = (uint64_t)__float_as_uint(t) << 32 | G.key_lo;
+  best = (ok && t > 0.001f && key < best) ? key : best;
+}
 template <int K>
 RTP_DEV void scan_kind_pf(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d, uint64_t& best, u16v& cur) {
+#if RTP_SCAN_PP
+  for (int q = b; q < e; q += 2) {
+    const u16v nxt = quad_head(sc, q + 1);
+    scan_one<K>(sc, q, cur, o, d, best);
+    if (q + 1 >= e) {
+      cur = nxt;
+      break;
+    }
+    cur = quad_head(sc, q + 2);
+    scan_one<K>(sc, q + 1, nxt, o, d, best);
+  }
+  return;
+#endif
   for (int q = b; q < e; q++) {
     const u16v nxt = quad_head(sc, q + 1);
     QuadGeom G;
@@ -341,14 +370,8 @@ RTP_DEV void pre_axis(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d,
   const float inv = __builtin_amdgcn_rcpf(comp<A>(d));
   const float oa = comp<A>(o);
   const f2v obc = f2v{comp<B>(o), comp<C>(o)}, dbc = f2v{comp<B>(d), comp<C>(d)};
-  for (int i = b; i < e; i++) {
-#if RTP_PRE_PF
-    const u8v nxt = pre_rec(sc, i + 1);
-    PreQuad P;
-    __builtin_memcpy(&P, &cur, sizeof(P));
-#else
-    const PreQuad& P = sc->pre[i];
-#endif
+  // the candidate key of one quad (~0u: not a candidate)
+  auto key_of = [&](const PreQuad& P) -> uint32_t {
     const float t = (P.x - oa) * inv;
     // the two in-plane coordinates as one packed FMA and one packed subtract
     const f2v u = __builtin_elementwise_fma(f2v{t, t}, dbc, obc) - f2v{P.cb, P.cc};
@@ -360,13 +383,28 @@ RTP_DEV void pre_axis(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d,
 #if RTP_PRE_ASM
     uint32_t key;
     asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(key) : "v"(__float_as_uint(t - m)), "v"(~31u), "s"((uint32_t)P.qpos));
-    key = ok ? key : ~0u;
+    return ok ? key : ~0u;
+#else
+    return ok ? ((__float_as_uint(t - m) & ~31u) | (uint32_t)P.qpos) : ~0u;
+#endif
+  };
+  auto fold = [&](uint32_t key) {  // keep the two smallest keys
+#if RTP_PRE_ASM
     asm("v_med3_u32 %0, %1, %2, %3" : "=v"(k2) : "v"(k1), "v"(k2), "v"(key));
 #else
-    const uint32_t key = ok ? ((__float_as_uint(t - m) & ~31u) | (uint32_t)P.qpos) : ~0u;
     k2 = min(k2, max(k1, key));
 #endif
     k1 = min(k1, key);
+  };
+  for (int i = b; i < e; i++) {
+#if RTP_PRE_PF
+    const u8v nxt = pre_rec(sc, i + 1);
+    PreQuad P;
+    __builtin_memcpy(&P, &cur, sizeof(P));
+#else
+    const PreQuad& P = sc->pre[i];
+#endif
+    fold(key_of(P));
 #if RTP_PRE_PF
     cur = nxt;
 #endif
@@ -1157,6 +1195,7 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
         frem -= 32;
       }
 #endif
+      const bool hash_now = mine;
 #pragma unroll
       for (int j = RTP_FF_EARLY ? 1 : 0; j < kFfTables; j++) {
         const uint32_t* __restrict__ tab = p.ff[j];
@@ -1167,7 +1206,7 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
       }
       int iters = 0;
       for (int i = 0;; i++) {
-        const bool act = mine && i < frem;
+        const bool act = hash_now && i < frem;
         if (!__any(act)) break;
         if (act) fseed = dead_step(fseed, t1, t2);
 #if RTP_DUP == 6
@@ -1181,11 +1220,9 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
         iters++;
       }
       bool again = false;
-      if (mine) {
-        s_seed[fslot] = fseed;
-        again = s_samples[fslot] < (uint32_t)S;
-      }
-      if (want_dbg) unfinished -= __popcll(__ballot(mine && !again));
+      if (mine) s_seed[fslot] = fseed;
+      if (hash_now) again = s_samples[fslot] < (uint32_t)S;
+      if (want_dbg) unfinished -= __popcll(__ballot(hash_now && !again));
 #if RTP_FAIR_READY
       // Fair share: a pixel whose completed samples are at or below the
       // wave's average (ff_tail / n_slots) goes to the FRONT of the READY
@@ -1213,11 +1250,16 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
         dbg[kDbgFfIters] += (unsigned long long)iters;
         dbg[kDbgCyclesFf] += __builtin_amdgcn_s_memtime() - t0;
       }
+#if !RTP_FF_FALL
       continue;
+#endif
+      // (RTP_FF_FALL: on into the refill, which takes the pixels this batch
+      // made READY, and the bounce: a sample's chain spends no iteration of
+      // its own on the fast-forward)
     }
     // ---- refill idle lanes with the next sample of READY pixels ----
     const unsigned long long tb = stamp(want_dbg);
-    const int take = min(n_idle, n_ready);
+    const int take = min(n_idle, ready_tail - ready_head);
     if (!has_path) {
       const int r = (int)lane_rank(idle);
       if (r < take) {
@@ -1257,7 +1299,7 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
       }
     }
     ready_head += take;
-    if (!__any(has_path)) break;  // nothing live, nothing READY, nothing to fast-forward
+    if (!__any(has_path) && ff_tail == ff_head) break;  // nothing live, nothing READY, nothing to fast-forward
     if (want_dbg) dbg[kDbgCyclesRefill] += __builtin_amdgcn_s_memtime() - tb;
     // ---- one depth of every live path ----
     bool ended = false;
