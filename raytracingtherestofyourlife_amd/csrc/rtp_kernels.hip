@@ -124,7 +124,7 @@ RTP_DEV u16v quad_head(const DevScene* __restrict__ sc, int q) {
   return reinterpret_cast<const u16v*>(sc->quads)[2 * min(q, kMaxQuads - 1)];
 }
 #ifndef RTP_SCAN_PP
-#define RTP_SCAN_PP 0  // ping-pong the two head registers (no copy of the prefetched head per quad)
+#define RTP_SCAN_PP 1  // ping-pong the two head registers (no copy of the prefetched head per quad)
 #endif
 template <int K>
 RTP_DEV void scan_one(const DevScene* __restrict__ sc, int q, const u16v& head, f3 o, f3 d, uint64_t& best) {
@@ -1360,7 +1360,8 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
       g = __shfl(g, 0) + (unsigned long long)(ff_tail - published);
       published = ff_tail;
       // completed fractions: global g / (npix*S) vs own ff_tail / (n_slots*S)
-      set_priority(((float)g / (float)p.npix - (float)ff_tail / (float)n_slots) / (float)S);
+      float lag = ((float)g / (float)p.npix - (float)ff_tail / (float)n_slots) / (float)S;
+      set_priority(lag);
     }
     if (want_dbg && unfinished < 64) {
       if (t_tail == 0) t_tail = __builtin_amdgcn_s_memtime();
