@@ -1015,6 +1015,17 @@ RTP_DEV void set_priority(float lag) {  // s_setprio needs an immediate
 // (after the 8-byte scene pointer; checked against the code object's
 // argument metadata by tests/test_abi.py)
 constexpr int kKParamsOffset = 8;
+typedef const __attribute__((address_space(4))) KParams CKP;
+// The kernel arguments re-read where they are used (scalar loads from the
+// kernarg segment): values loaded once and kept live through the scheduling
+// loop were SGPRs spilled to VGPR lanes (v_readlane in the hot path).
+RTP_DEV CKP& kparams() {
+  CKP* pp = (CKP*)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() +
+                   kKParamsOffset);
+  asm volatile("" : "+s"(pp));
+  return *pp;
+}
+typedef const __attribute__((address_space(1))) uint32_t GU32;
 template <bool kStats, bool kBvh, bool kTiles = false>
 #if RTP_POOL_MAX_VGPR > 0
 #define RTP_POOL_VGPR_ATTR __attribute__((amdgpu_num_vgpr(RTP_POOL_MAX_VGPR)))
@@ -1127,10 +1138,11 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
       // the 32-depth table
       uint32_t early = 0;
       const int frc = frem & kRemMask;
-      const bool has_direct = mine && p.ffd != nullptr && (unsigned)(frc - p.ffd_first) < (unsigned)p.ffd_count;
-      const bool has_early = mine && !has_direct && p.ff[0] != nullptr && frc >= 32;
+      CKP& FP = kparams();
+      const bool has_direct = mine && FP.ffd != nullptr && (unsigned)(frc - FP.ffd_first) < (unsigned)FP.ffd_count;
+      const bool has_early = mine && !has_direct && FP.ff[0] != nullptr && frc >= 32;
       if (has_direct || has_early) {
-        const uint32_t* src = has_direct ? p.ffd + ((uint64_t)(frc - p.ffd_first) << 32) : p.ff[0];
+        GU32* src = (GU32*)(has_direct ? FP.ffd + ((uint64_t)(frc - FP.ffd_first) << 32) : FP.ff[0]);
         early = src[fseed];
       }
 #endif
@@ -1198,7 +1210,7 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
       const bool hash_now = mine;
 #pragma unroll
       for (int j = RTP_FF_EARLY ? 1 : 0; j < kFfTables; j++) {
-        const uint32_t* __restrict__ tab = p.ff[j];
+        GU32* __restrict__ tab = (GU32*)kparams().ff[j];
         if (tab != nullptr && mine && frem >= (32 >> j)) {
           fseed = tab[fseed];
           frem -= 32 >> j;
@@ -1270,14 +1282,10 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
 #endif
 #if RTP_CAM_RELOAD
         // the camera and tile constants re-read from the kernel arguments
-        // here (scalar loads): kept live through the loop they were SGPRs
-        // spilled to VGPR lanes, ~30 v_readlane per refill
-        // (through the kernarg segment pointer: &p would copy p to scratch)
-        typedef const __attribute__((address_space(4))) KParams CKP;
-        CKP* pp = (CKP*)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() +
-                         kKParamsOffset);
-        asm volatile("" : "+s"(pp));
-        CKP& P = *pp;
+        // here (kparams): kept live through the loop they were SGPRs spilled
+        // to VGPR lanes, ~30 v_readlane per refill (through the kernarg
+        // segment pointer: &p would copy p to scratch)
+        CKP& P = kparams();
 #else
         const KParams& P = p;
 #endif
@@ -1356,11 +1364,11 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
     if (RTP_PRIO_BALANCE && ff_tail - published >= kPrioPeriod) {
       // ff_tail counts this wave's finished samples
       unsigned long long g = 0;
-      if (lane == 0) g = atomicAdd(p.progress, (unsigned long long)(ff_tail - published));
+      if (lane == 0) g = atomicAdd(kparams().progress, (unsigned long long)(ff_tail - published));
       g = __shfl(g, 0) + (unsigned long long)(ff_tail - published);
       published = ff_tail;
       // completed fractions: global g / (npix*S) vs own ff_tail / (n_slots*S)
-      float lag = ((float)g / (float)p.npix - (float)ff_tail / (float)n_slots) / (float)S;
+      float lag = ((float)g / (float)kparams().npix - (float)ff_tail / (float)n_slots) / (float)S;
       set_priority(lag);
     }
     if (want_dbg && unfinished < 64) {
