@@ -12,6 +12,9 @@
 #include "rtp_layout.hpp"
 
 #define RTP_DEV __device__ __forceinline__
+#ifndef RTP_MIN3_ACCEPT
+#define RTP_MIN3_ACCEPT 1  // the parallelogram test's sign checks as one min3 and one compare
+#endif
 #ifndef RTP_PARA_BITWISE
 #define RTP_PARA_BITWISE 1
 #endif
@@ -360,7 +363,14 @@ RTP_DEV bool quad_hit_masked(const G& Q, const DevQuad& M, f3 o, f3 d, float& t_
     // ap < 0 <=> -al2.y < 0 <=> al2.y > 0 (NaN: false both ways; -(+-0) is
     // not < 0 and +-0 is not > 0), likewise bp; evaluated without short
     // circuits so no lane mask or max canonicalisation is generated
+#if RTP_MIN3_ACCEPT
+    // !(a < 0) & !(b < 0) & !(c < 0) == !(minNum(a, b, c) < 0): minNum skips
+    // NaN operands, whose terms are true (!(NaN < 0)); all three NaN gives
+    // NaN, true as well; -0 is not < 0 either way (no signaling NaNs arise)
+    const bool ok1 = !(fabsf(det) < kEps) & !(fminf(fminf(alpha, beta), t) < 0.0f);
+#else
     const bool ok1 = !(fabsf(det) < kEps) & !(alpha < 0.0f) & !(beta < 0.0f) & !(t < 0.0f);
+#endif
     const bool second = (alpha + beta) > 1.0f;
     const bool bad2 = (al2.y > 0.0f) | (be2.y > 0.0f);
     t_out = t;

@@ -126,27 +126,46 @@ RTP_DEV u16v quad_head(const DevScene* __restrict__ sc, int q) {
 #ifndef RTP_SCAN_PP
 #define RTP_SCAN_PP 1  // ping-pong the two head registers (no copy of the prefetched head per quad)
 #endif
+#ifndef RTP_SCAN_PTR
+#define RTP_SCAN_PTR 1  // walk the quads with a pointer (2 SALU per prefetch address, not ~7)
+#endif
 template <int K>
-RTP_DEV void scan_one(const DevScene* __restrict__ sc, int q, const u16v& head, f3 o, f3 d, uint64_t& best) {
+RTP_DEV void scan_one(const DevQuad& M, const u16v& head, f3 o, f3 d, uint64_t& best) {
   QuadGeom G;
   __builtin_memcpy(&G, &head, sizeof(G));
   float t;
-  const bool ok = quad_hit_masked<K>(G, sc->quads[q], o, d, t);
+  const bool ok = quad_hit_masked<K>(G, M, o, d, t);
   const uint64_t key = (uint64_t)__float_as_uint(t) << 32 | G.key_lo;
   best = (ok && t > 0.001f && key < best) ? key : best;
 }
+RTP_DEV u16v head_at(const DevQuad* q) { return *reinterpret_cast<const u16v*>(q); }
 template <int K>
 RTP_DEV void scan_kind_pf(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d, uint64_t& best, u16v& cur) {
-#if RTP_SCAN_PP
+#if RTP_SCAN_PP && RTP_SCAN_PTR
+  // (the prefetches read at most two records past quads[] -- still inside
+  // DevScene, whose spheres[] follow -- and those values are never used)
+  const DevQuad* qp = sc->quads + b;
+  for (int n = e - b; n > 0; n -= 2, qp += 2) {
+    const u16v nxt = head_at(qp + 1);
+    scan_one<K>(qp[0], cur, o, d, best);
+    if (n == 1) {
+      cur = nxt;
+      break;
+    }
+    cur = head_at(qp + 2);
+    scan_one<K>(qp[1], nxt, o, d, best);
+  }
+  return;
+#elif RTP_SCAN_PP
   for (int q = b; q < e; q += 2) {
     const u16v nxt = quad_head(sc, q + 1);
-    scan_one<K>(sc, q, cur, o, d, best);
+    scan_one<K>(sc->quads[q], cur, o, d, best);
     if (q + 1 >= e) {
       cur = nxt;
       break;
     }
     cur = quad_head(sc, q + 2);
-    scan_one<K>(sc, q + 1, nxt, o, d, best);
+    scan_one<K>(sc->quads[q + 1], nxt, o, d, best);
   }
   return;
 #endif
@@ -396,6 +415,26 @@ RTP_DEV void pre_axis(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d,
 #endif
     k1 = min(k1, key);
   };
+#if RTP_PRE_PF && RTP_SCAN_PTR
+  // ping-pong heads, pointer walk (as scan_kind_pf; prefetches past pre[]
+  // stay inside DevScene: prex[] follows)
+  auto as_pre = [](const u8v& v) {
+    PreQuad P;
+    __builtin_memcpy(&P, &v, sizeof(P));
+    return P;
+  };
+  const PreQuad* pq = sc->pre + b;
+  for (int n = e - b; n > 0; n -= 2, pq += 2) {
+    const u8v nxt = *reinterpret_cast<const u8v*>(pq + 1);
+    fold(key_of(as_pre(cur)));
+    if (n == 1) {
+      cur = nxt;
+      break;
+    }
+    cur = *reinterpret_cast<const u8v*>(pq + 2);
+    fold(key_of(as_pre(nxt)));
+  }
+#else
   for (int i = b; i < e; i++) {
 #if RTP_PRE_PF
     const u8v nxt = pre_rec(sc, i + 1);
@@ -409,6 +448,7 @@ RTP_DEV void pre_axis(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d,
     cur = nxt;
 #endif
   }
+#endif
 }
 
 // quad_hit_masked<K>'s parallelogram path for an axis-plane quad of any of
@@ -448,7 +488,11 @@ RTP_DEV bool quad_hit_axis(const PreExact& E, f3 o, f3 d, float& t_out) {
   const f2v Qa = -(Tj * E.bs);                    // -s * T_j b
   const f2v be2 = (f2v{dj, dj} * Qj + f2v{da, da} * Qa) * inv_det;  // (beta, -bp)
   const float t = (E.c * Qj.x) * inv_det;
+#if RTP_MIN3_ACCEPT
+  const bool ok1 = !(fabsf(det) < kEps) & !(fminf(fminf(al2.x, be2.x), t) < 0.0f);  // (see quad_hit_masked)
+#else
   const bool ok1 = !(fabsf(det) < kEps) & !(al2.x < 0.0f) & !(be2.x < 0.0f) & !(t < 0.0f);
+#endif
   const bool second = (al2.x + be2.x) > 1.0f;
   const bool bad2 = (al2.y > 0.0f) | (be2.y > 0.0f);
   t_out = t;

@@ -175,6 +175,14 @@ struct alignas(16) DevScene {
   PreQuad pre[kMaxPre];
   PreExact prex[kMaxPre];  // by quad position (< n_pre)
 };
+// The pool kernel's scans prefetch up to two records past the last quad or
+// prefilter record; these must stay inside DevScene (values never used).
+static_assert(offsetof(DevScene, spheres) == offsetof(DevScene, quads) + sizeof(DevQuad) * kMaxQuads &&
+                  sizeof(DevSphere) * kMaxSpheres >= 2 * sizeof(DevQuad),
+              "quads[] is followed by at least two quads' worth of DevScene");
+static_assert(offsetof(DevScene, prex) == offsetof(DevScene, pre) + sizeof(PreQuad) * kMaxPre &&
+                  sizeof(PreExact) * kMaxPre >= 2 * sizeof(PreQuad),
+              "pre[] is followed by at least two records' worth of DevScene");
 
 // camera constants (Camera.cxx:437-474): eye, nlook, delta_x, delta_y
 struct DevCamera {
