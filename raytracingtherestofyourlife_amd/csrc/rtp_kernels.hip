@@ -554,6 +554,22 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
 #endif
   };
   bool full = true;  // this lane needs the exact scan of the axis-plane quads (kinds 1..6)
+#if RTP_DUP == 15
+  {  // cost attribution: the exact scan of kinds 7..10 and 0 once more, on an opaque origin
+    f3 o2 = o;
+    RTP_OPQ(o2.x);
+    uint64_t k2 = kNoHitKey;
+    const int g6 = sc->kind_begin[6], g7 = sc->kind_begin[7], g8 = sc->kind_begin[8], g9 = sc->kind_begin[9],
+              g10 = sc->kind_begin[10], g11 = sc->kind_begin[11];
+    u16v cur = quad_head(sc, g6);
+    scan_kind_pf<7>(sc, g6, g7, o2, d, k2, cur);
+    scan_kind_pf<8>(sc, g7, g8, o2, d, k2, cur);
+    scan_kind_pf<9>(sc, g8, g9, o2, d, k2, cur);
+    scan_kind_pf<10>(sc, g9, g10, o2, d, k2, cur);
+    scan_kind_pf<0>(sc, g10, g11, o2, d, k2, cur);
+    if ((uint32_t)k2 == 0x12345u) key ^= 1;
+  }
+#endif
 #if RTP_PREFILTER
   const bool pre = prefilter && sc->n_pre > 0;  // wave-uniform
 #if !RTP_PREX_EARLY
