@@ -959,6 +959,40 @@ RTP_DEV int64_t tile_pixel(const KP& p, int k) {
   const int tx = ti - ty * p.tile_tx;
   return (int64_t)(ty * 16 + (within >> 4)) * p.nx + tx * 16 + (within & 15);
 }
+// The pixel's column and row directly (refill): the tile deal gives them
+// without forming the linear index; a pixel index is split by a float
+// reciprocal quotient with one correction each way, exact while every index
+// is below 2^24 (the estimate is then off by at most one), else by integer
+// division (a wave-uniform branch).  The compiler's signed % and / cost ~40
+// VALU per refill.
+#ifndef RTP_PIXEL_XY
+#define RTP_PIXEL_XY 1
+#endif
+template <bool kTiles = false, class KP>
+RTP_DEV void pixel_xy(const KP& p, int k, int& pi, int& pj) {
+  if constexpr (kTiles) {
+    const int ti = (k >> 8) * p.tile_world + p.tile_rank, within = k & 255;
+    int ty = (int)((float)ti * __builtin_amdgcn_rcpf((float)p.tile_tx));
+    ty += (ty + 1) * p.tile_tx <= ti;
+    ty -= ty * p.tile_tx > ti;
+    const int tx = ti - ty * p.tile_tx;
+    pj = ty * 16 + (within >> 4);
+    pi = tx * 16 + (within & 15);
+  } else {
+    const int u = (int)(p.pixel_ids ? p.pixel_ids[k] : p.pixel_begin + k);  // in [0, nx * ny)
+    const int nx = p.nx;
+    if ((int64_t)nx * p.ny <= (int64_t)1 << 24) {
+      int q = (int)((float)u * __builtin_amdgcn_rcpf((float)nx));
+      q += (q + 1) * nx <= u;
+      q -= q * nx > u;
+      pj = q;
+      pi = u - q * nx;
+    } else {
+      pj = (int)((uint32_t)u / (uint32_t)nx);
+      pi = u - pj * nx;
+    }
+  }
+}
 // kTiles: a separate kernel instance (rtp_render_tiles_device).  A runtime
 // branch here changed the compiler's code for the whole scheduling loop of
 // the other modes (+9% time), as other additions to the refill path did.
@@ -1302,8 +1336,13 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
       // paths, back sooner) take more than their share of lanes, so the
       // expensive pixels' sequential sample chains ran on alone at the end
       // (17% of bounce steps with ~12 of 64 lanes live).
+#if RTP_URGENT_PERMILLE == 0
+      // (samples * n_slots <= 2^23 * 2^8 and ff_tail <= n_slots * spp: 32 bits suffice)
+      const bool urgent = again && s_samples[fslot] * (uint32_t)n_slots <= (uint32_t)ff_tail;
+#else
       const bool urgent = again && (uint64_t)s_samples[fslot] * (uint64_t)n_slots * 1000u <=
                                        (uint64_t)ff_tail * (uint64_t)(1000 + RTP_URGENT_PERMILLE);
+#endif
       const uint64_t pu = __ballot(urgent), pn = __ballot(again && !urgent);
       ready_head -= __popcll(pu);
       if (urgent) q_ready[(ready_head + (int)lane_rank(pu)) & (kPool - 1)] = (uint16_t)fslot;
@@ -1349,8 +1388,13 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
 #else
         const KParams& P = p;
 #endif
+#if RTP_PIXEL_XY
+        int pi, pj;
+        pixel_xy<kTiles>(P, slot * n_waves + w, pi, pj);  // (32-bit index: a 64-bit one spilled)
+#else
         const int64_t pix = pixel_of<kTiles>(P, slot * n_waves + w);  // (32-bit: a 64-bit index spilled)
         const int pi = (int32_t)pix % P.nx, pj = (int32_t)pix / P.nx;
+#endif
         ps.dir = camera_ray(P.cam, pi, pj, P.nx, P.ny, seed);
 #if RTP_DUP == 7
         {
@@ -1415,8 +1459,9 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
     // RTP_CRIT_FF/1000 runs its sample chain on the critical path (its path
     // length keeps it behind): its fast-forward is not left waiting for the
     // READY queue to run dry -- the batch runs in the next iteration.
-    if (__ballot(ended && (uint64_t)s_samples[slot] * (uint64_t)n_slots * 1000u <
-                              (uint64_t)ff_tail * (uint64_t)(1000 - RTP_CRIT_FF)))
+    // (a scheduling heuristic: single precision is plenty)
+    if (__ballot(ended && (float)(s_samples[slot] * (uint32_t)n_slots) * 1000.0f <
+                              (float)ff_tail * (float)(1000 - RTP_CRIT_FF)))
       critical_ff = true;
 #endif
     ff_tail += __popcll(fin);

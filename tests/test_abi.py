@@ -112,3 +112,34 @@ def test_package_refuses_to_run_without_library(tmp_path, monkeypatch):
     monkeypatch.setattr(L, "_lib", None)
     with pytest.raises(RuntimeError):
         L.load(build_if_missing=False)
+
+
+def test_pool_kernel_reads_kparams_at_its_kernarg_offset(tmp_path):
+    """rtp_render_pool re-reads KParams through the kernarg segment pointer at
+    byte offset kKParamsOffset = 8 (rtp_kernels.hip kparams()): check that
+    against the argument metadata of the gfx950 code object in librtp.so."""
+    import shutil
+
+    import raytracingtherestofyourlife_amd as rtp
+
+    llvm = "/opt/rocm/lib/llvm/bin"
+    tools = [shutil.which("objcopy"), os.path.join(llvm, "clang-offload-bundler"), os.path.join(llvm, "llvm-readelf")]
+    if not all(t and os.path.exists(t) for t in tools):
+        pytest.skip("objcopy / clang-offload-bundler / llvm-readelf not available")
+    fat, co = str(tmp_path / "fat.bin"), str(tmp_path / "co.o")
+    subprocess.run([tools[0], "--dump-section", f".hip_fatbin={fat}", rtp.LIB_PATH], check=True, capture_output=True)
+    subprocess.run([tools[1], "--type=o", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fat}",
+                    f"--output={co}", "--unbundle"], check=True, capture_output=True)
+    notes = subprocess.run([tools[2], "--notes", co], check=True, capture_output=True, text=True).stdout
+    blocks = re.split(r"\n\s*-?\s*\.args:", notes)
+    seen = 0
+    for i in range(1, len(blocks)):
+        # the kernel a .args list belongs to: the next .name after it
+        name = re.search(r"\.name:\s+(\S+)", blocks[i])
+        if not name or "rtp_render_pool" not in name.group(1):
+            continue
+        offsets = [int(x) for x in re.findall(r"\.offset:\s+(\d+)", blocks[i].split(".name:")[0])]
+        sizes = [int(x) for x in re.findall(r"\.size:\s+(\d+)", blocks[i].split(".name:")[0])]
+        assert offsets[:2] == [0, 8] and sizes[1] >= 200, (name.group(1), offsets[:3], sizes[:3])
+        seen += 1
+    assert seen >= 6, f"found {seen} rtp_render_pool kernels"
