@@ -741,7 +741,13 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
   const f3 org = ps.org, dir = ps.dir;
   const int d = ps.d;
   // intersect + CollectIntersecttWorklet (SurfaceWorklets.h:104-109)
-  Hit h = closest_hit<kBvh>(sc, org, dir, true);
+  uint32_t fb = 0;  // (stats) 1: this lane ran the exact scan of the prefiltered quads
+  Hit h = closest_hit<kBvh>(sc, org, dir, true, st ? &fb : nullptr);
+  if (st) {
+    const unsigned long long m = __ballot(fb == 1u);
+    dbg[kDbgFallbackSteps] += m ? 1 : 0;
+    dbg[kDbgFallbackLanes] += (unsigned long long)__popcll(m);
+  }
 #if RTP_DUP == 1
   {
     f3 o2 = org;

@@ -259,6 +259,8 @@ enum DbgCounter {
   kDbgTailSteps,         // bounce steps taken while < 64 of the wave's pixels were unfinished
   kDbgTailLanes,         // live lanes summed over those steps
   kDbgTailCycles,        // s_memtime cycles from the first such step to the wave's end
+  kDbgFallbackSteps,     // bounce steps in which some lane ran the exact scan of the prefiltered quads
+  kDbgFallbackLanes,     // lanes that did, summed over all bounce steps
   kDbgCounters
 };
 

@@ -325,7 +325,7 @@ class Device:
     DEBUG_COUNTERS = ("bounce_steps", "bounce_lanes", "ff_phases", "ff_lanes", "ff_iters", "cycles_bounce",
                       "cycles_ff", "cycles_total", "cycles_intersect", "cycles_bounce_call", "cycles_end",
                       "cycles_refill", "real_start", "real_end", "hw_id", "tail_steps", "tail_lanes",
-                      "tail_cycles", "max_wave_cycles")
+                      "tail_cycles", "fallback_steps", "fallback_lanes", "max_wave_cycles")
 
     def debug_counters(self) -> dict:
         """Pool-kernel counters of the last launch made with RTP_DEBUG_STATS=1."""

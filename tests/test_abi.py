@@ -127,7 +127,11 @@ def test_pool_kernel_reads_kparams_at_its_kernarg_offset(tmp_path):
     if not all(t and os.path.exists(t) for t in tools):
         pytest.skip("objcopy / clang-offload-bundler / llvm-readelf not available")
     fat, co = str(tmp_path / "fat.bin"), str(tmp_path / "co.o")
-    subprocess.run([tools[0], "--dump-section", f".hip_fatbin={fat}", rtp.LIB_PATH], check=True, capture_output=True)
+    # (on a copy: objcopy without an output file rewrites its input in place,
+    # which would replace the loaded product library under the running process)
+    lib = str(tmp_path / "librtp_copy.so")
+    shutil.copyfile(rtp.LIB_PATH, lib)
+    subprocess.run([tools[0], "--dump-section", f".hip_fatbin={fat}", lib], check=True, capture_output=True)
     subprocess.run([tools[1], "--type=o", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fat}",
                     f"--output={co}", "--unbundle"], check=True, capture_output=True)
     notes = subprocess.run([tools[2], "--notes", co], check=True, capture_output=True, text=True).stdout

@@ -33,7 +33,9 @@ c.update(kernel_ms=st.kernel_ms, samples=samples, live_bounces=L,
          per_step_refill=c["cycles_refill"] / max(1, c["bounce_steps"]),
          tail_frac_steps=c["tail_steps"] / max(1, c["bounce_steps"]),
          tail_lanes_per_step=c["tail_lanes"] / max(1, c["tail_steps"]),
-         tail_frac_cycles=c["tail_cycles"] / max(1, c["cycles_total"]))
+         tail_frac_cycles=c["tail_cycles"] / max(1, c["cycles_total"]),
+         fallback_frac_steps=c["fallback_steps"] / max(1, c["bounce_steps"]),
+         fallback_lanes_per_step=c["fallback_lanes"] / max(1, c["bounce_steps"]))
 print(json.dumps(c, indent=1))
 rec = dev.debug_wave_records()
 import numpy as np
