@@ -56,7 +56,7 @@
 #define RTP_FF_EARLY 1  // pool kernel: first jump-table read overlapped with the radiance loads
 #endif
 #ifndef RTP_FF_FALL
-#define RTP_FF_FALL 0  // pool kernel: a fast-forward batch is followed by refill + bounce in the same iteration
+#define RTP_FF_FALL 1  // pool kernel: a fast-forward batch is followed by refill + bounce in the same iteration
 #endif
 #ifndef RTP_FF_MARGIN
 #define RTP_FF_MARGIN 12  // pool kernel: fast-forward when READY holds fewer than idle lanes + this
