@@ -12,6 +12,7 @@ ap.add_argument("--spp", type=int, default=50)
 ap.add_argument("--depth", type=int, default=50)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--variant", type=int, default=0)
+ap.add_argument("--tiles", action="store_true", help="the tile-deal instance bench.py runs (rank 0 of 1), no live counters")
 a = ap.parse_args()
 dev = rtp.Device(0)
 dev.set_cornell_box(a.variant)
@@ -22,7 +23,11 @@ live = torch.zeros(n, dtype=torch.int32, device="cuda")
 s = torch.cuda.current_stream().cuda_stream
 for r in range(a.reps):
     t = time.time()
-    st = dev.render_device(cam, a.nx, a.ny, a.spp, a.depth, out.data_ptr(), stream=s, live_ptr=live.data_ptr(), timed=True)
+    if a.tiles:
+        st = dev.render_tiles_device(cam, a.nx, a.ny, a.spp, a.depth, out.data_ptr(), 0, 1, stream=s, timed=True)
+    else:
+        st = dev.render_device(cam, a.nx, a.ny, a.spp, a.depth, out.data_ptr(), stream=s, live_ptr=live.data_ptr(),
+                               timed=True)
     torch.cuda.synchronize()
     wall = time.time() - t
     L = live.to(torch.int64).sum().item() / (n * a.spp)
