@@ -13,7 +13,15 @@ ap.add_argument("--depth", type=int, default=50)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--variant", type=int, default=0)
 ap.add_argument("--tiles", action="store_true", help="the tile-deal instance bench.py runs (rank 0 of 1), no live counters")
+ap.add_argument("--list-tiles", action="store_true", help="the pixel-list path over the tile deal's order")
+ap.add_argument("--list-contig", action="store_true", help="the pixel-list path over the contiguous order")
 a = ap.parse_args()
+ids = None
+if a.list_contig:
+    ids = torch.arange(a.nx * a.ny, dtype=torch.int64, device="cuda")
+if a.list_tiles:
+    from raytracingtherestofyourlife_amd import shard
+    ids = torch.from_numpy(shard.tile_pixels(a.nx, a.ny, 0, 1)).cuda()
 dev = rtp.Device(0)
 dev.set_cornell_box(a.variant)
 cam = rtp.default_camera()
@@ -23,7 +31,10 @@ live = torch.zeros(n, dtype=torch.int32, device="cuda")
 s = torch.cuda.current_stream().cuda_stream
 for r in range(a.reps):
     t = time.time()
-    if a.tiles:
+    if ids is not None:
+        st = dev.render_device(cam, a.nx, a.ny, a.spp, a.depth, out.data_ptr(), pixel_count=n, pixel_ids_ptr=ids.data_ptr(),
+                               stream=s, live_ptr=live.data_ptr(), timed=True)
+    elif a.tiles:
         st = dev.render_tiles_device(cam, a.nx, a.ny, a.spp, a.depth, out.data_ptr(), 0, 1, stream=s, timed=True)
     else:
         st = dev.render_device(cam, a.nx, a.ny, a.spp, a.depth, out.data_ptr(), stream=s, live_ptr=live.data_ptr(),
