@@ -12,12 +12,6 @@
 #include "rtp_layout.hpp"
 
 #define RTP_DEV __device__ __forceinline__
-#ifndef RTP_MIN3_ACCEPT
-#define RTP_MIN3_ACCEPT 1  // the parallelogram test's sign checks as one min3 and one compare
-#endif
-#ifndef RTP_PARA_BITWISE
-#define RTP_PARA_BITWISE 1
-#endif
 
 namespace rtp {
 
@@ -111,11 +105,7 @@ RTP_DEV float rsqrt_exact(float x) {  // 1 / sqrtf(x)  (vtkm::RMagnitude, CPU bu
 // 1/det of the quad tests.  The reciprocal is only used when !(|det| < kEps)
 // (kEps = 1e-5 > 2^-40), so the small end of fast_range never matters: only
 // |det| > 2^40 (or NaN) takes the IEEE path.
-#ifndef RTP_RCP_DET_FAST
-#define RTP_RCP_DET_FAST 1
-#endif
 RTP_DEV float rcp_det(float x) {
-#if RTP_RCP_DET_FAST
   float r = rcp_nr1(x);
   const bool slow = !(fabsf(x) <= 0x1p40f);
   if (__ballot(slow)) {
@@ -123,9 +113,6 @@ RTP_DEV float rcp_det(float x) {
     if (slow) r = 1.0f / x;
   }
   return r;
-#else
-  return rcp_exact(x);
-#endif
 }
 // vtkm::RMagnitude on the CPU build: 1 / sqrt(x.x)
 RTP_DEV float rmag(f3 a) { return rsqrt_exact(dot(a, a)); }
@@ -359,30 +346,17 @@ RTP_DEV bool quad_hit_masked(const G& Q, const DevQuad& M, f3 o, f3 d, float& t_
     const float Qv[3] = {Q2[0].x, Q2[1].x, Q2[2].x};
     const float t = dot_m<M03 & MQ>(Q.e03, Qv) * inv_det;
     const float alpha = al2.x, beta = be2.x;
-#if RTP_PARA_BITWISE
     // ap < 0 <=> -al2.y < 0 <=> al2.y > 0 (NaN: false both ways; -(+-0) is
     // not < 0 and +-0 is not > 0), likewise bp; evaluated without short
-    // circuits so no lane mask or max canonicalisation is generated
-#if RTP_MIN3_ACCEPT
+    // circuits so no lane mask or max canonicalisation is generated;
     // !(a < 0) & !(b < 0) & !(c < 0) == !(minNum(a, b, c) < 0): minNum skips
     // NaN operands, whose terms are true (!(NaN < 0)); all three NaN gives
     // NaN, true as well; -0 is not < 0 either way (no signaling NaNs arise)
     const bool ok1 = !(fabsf(det) < kEps) & !(fminf(fminf(alpha, beta), t) < 0.0f);
-#else
-    const bool ok1 = !(fabsf(det) < kEps) & !(alpha < 0.0f) & !(beta < 0.0f) & !(t < 0.0f);
-#endif
     const bool second = (alpha + beta) > 1.0f;
     const bool bad2 = (al2.y > 0.0f) | (be2.y > 0.0f);
     t_out = t;
     return ok1 & !(second & bad2);
-#else
-    const float ap = -al2.y, bp = -be2.y;
-    bool ok = !(fabsf(det) < kEps) && !(alpha < 0.0f) && !(beta < 0.0f) && !(t < 0.0f);
-    const bool second = (alpha + beta) > 1.0f;
-    ok = ok && (!second || (!(ap < 0.0f) && !(bp < 0.0f)));
-    t_out = t;
-    return ok;
-#endif
   }
   const float T[3] = {o.x - Q.vv[0][0], o.y - Q.vv[1][0], o.z - Q.vv[2][0]};
   const float alpha = dot_m<MP>(T, P) * inv_det;
@@ -505,14 +479,7 @@ RTP_DEV float sphere_pdf_value(const DevLights& L, f3 o, f3 v, float ctm = -1.0f
 // polynomial constants out of the render loop into ~30 VGPRs held for the
 // whole kernel (and spills around them); as a call they live only in the
 // callee, which runs on dielectric hits alone.
-#ifndef RTP_POW_NOINLINE
-#define RTP_POW_NOINLINE 1
-#endif
-#if RTP_POW_NOINLINE
 __device__ __attribute__((noinline)) double pow5(double x) { return pow(x, 5.0); }
-#else
-RTP_DEV double pow5(double x) { return pow(x, 5.0); }
-#endif
 RTP_DEV float schlick(float cosine, float ref_idx) {
   float r0 = (1 - ref_idx) / (1 + ref_idx);
   r0 = r0 * r0;

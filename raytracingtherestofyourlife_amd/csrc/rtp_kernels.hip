@@ -32,46 +32,15 @@
 
 #include "rtp_device.hpp"
 
-// Cost attribution (development builds only, RTP_DUP=n): component n is
-// computed a second time on opaque copies of its inputs and its result only
-// feeds a branch that cannot be taken, so the render is unchanged and
-// T(RTP_DUP=n) - T(base) is that component's marginal cost.
-#ifndef RTP_DUP
-#define RTP_DUP 0
-#endif
-#define RTP_OPQ(x) asm volatile("" : "+v"(x))
-#define RTP_SINK(v, s) \
-  if (__float_as_uint(v) == 0x7fc12345u) (s) ^= 1u
-
-#ifndef RTP_FAIR_READY
-#define RTP_FAIR_READY 1  // pool kernel: lagging pixels jump the READY queue
-#endif
-#ifndef RTP_DEFER_RADIANCE
-#define RTP_DEFER_RADIANCE 1  // pool kernel: radiance product in the fast-forward batch
-#endif
-#ifndef RTP_REUSE_CTM
-#define RTP_REUSE_CTM 1  // sphere pdf reuses the light-sphere generator's cos_theta_max
-#endif
-#ifndef RTP_FF_EARLY
-#define RTP_FF_EARLY 1  // pool kernel: first jump-table read overlapped with the radiance loads
-#endif
-#ifndef RTP_FF_FALL
-#define RTP_FF_FALL 1  // pool kernel: a fast-forward batch is followed by refill + bounce in the same iteration
-#endif
+// One compiled path.  The alternatives measured and rejected in rounds 1-2
+// (and the RTP_DUP cost-attribution probes behind DESIGN.md 4.1's tables) are
+// in git history: `git show c9f7859:raytracingtherestofyourlife_amd/csrc/
+// rtp_kernels.hip`.  The numeric scheduling constants below stay tunable.
 #ifndef RTP_FF_MARGIN
 #define RTP_FF_MARGIN 12  // pool kernel: fast-forward when READY holds fewer than idle lanes + this
 #endif
-#ifndef RTP_URGENT_PERMILLE
-#define RTP_URGENT_PERMILLE 0  // pool kernel: READY front for pixels at most this far above the average samples
-#endif
 #ifndef RTP_CRIT_FF
 #define RTP_CRIT_FF 100  // pool kernel: lag (per mille of the wave's average samples) that makes a pixel critical
-#endif
-#ifndef RTP_CAM_RELOAD
-#define RTP_CAM_RELOAD 1  // pool kernel: refill reads the camera from the kernel arguments, not from spilled SGPRs
-#endif
-#ifndef RTP_MERGED_GEN
-#define RTP_MERGED_GEN 1  // branch-free generator pass (bounce); 0: the three divergent branches
 #endif
 
 namespace rtp {
@@ -90,45 +59,24 @@ struct Hit {
 // returns the lexicographic minimum of (t, index) over the hits, so the quads
 // can be visited grouped by zero-structure kind (one tight loop per kind) as
 // long as equal t is broken by the original index.
-#ifndef RTP_HIT_KEY
-#define RTP_HIT_KEY 1
-#endif
-#if RTP_HIT_KEY
 // The (t, orig) minimum as one unsigned 64-bit key {bits(t), orig << 8 | q}:
 // an accepted t is > 0.001, and positive floats order like their bit
 // patterns, so key order is exactly "t, then reference index".  The scan
 // position q rides in the low bits (orig is unique, so it never decides).
 static_assert(kMaxQuads <= 256, "key_lo packs orig and the scan position in 8 bits each");
 constexpr uint64_t kNoHitKey = (uint64_t)0x7f7fffffu << 32 | 0xffffffffu;  // {FLT_MAX, none}
-template <int K>
-RTP_DEV void scan_kind(const DevScene* __restrict__ sc, int g, f3 o, f3 d, uint64_t& best) {
-  const int b = sc->kind_begin[g], e = sc->kind_begin[g + 1];
-  for (int q = b; q < e; q++) {
-    const DevQuad& Q = sc->quads[q];
-    float t;
-    const bool ok = quad_hit_masked<K>(Q, Q, o, d, t);
-    const uint64_t key = (uint64_t)__float_as_uint(t) << 32 | Q.key_lo;
-    best = (ok && t > 0.001f && key < best) ? key : best;
-  }
-}
-// The same scan with the quads' 64-byte scan heads (QuadGeom) fetched as one
+// The scan reads the quads' 64-byte scan heads (QuadGeom) as one
 // s_load_dwordx16 each, the NEXT quad's issued before the current one is
 // tested, so its scalar-load latency hides behind the test's VALU work (the
 // field-by-field loads compiled to ~5 dependent s_load / s_waitcnt round
-// trips per quad).  `cur` holds quad b's head on entry and quad e's (the next
-// group's first: the groups are contiguous in scan order) on exit.
-#ifndef RTP_SCAN_PF
-#define RTP_SCAN_PF 1
-#endif
+// trips per quad).  The two head registers ping-pong (no copy of the
+// prefetched head per quad) and the walk is a pointer (2 SALU per prefetch
+// address, not ~7 for a clamped index).  `cur` holds quad b's head on entry
+// and quad e's (the next group's first: the groups are contiguous in scan
+// order) on exit.
 RTP_DEV u16v quad_head(const DevScene* __restrict__ sc, int q) {
   return reinterpret_cast<const u16v*>(sc->quads)[2 * min(q, kMaxQuads - 1)];
 }
-#ifndef RTP_SCAN_PP
-#define RTP_SCAN_PP 1  // ping-pong the two head registers (no copy of the prefetched head per quad)
-#endif
-#ifndef RTP_SCAN_PTR
-#define RTP_SCAN_PTR 1  // walk the quads with a pointer (2 SALU per prefetch address, not ~7)
-#endif
 template <int K>
 RTP_DEV void scan_one(const DevQuad& M, const u16v& head, f3 o, f3 d, uint64_t& best) {
   QuadGeom G;
@@ -141,7 +89,6 @@ RTP_DEV void scan_one(const DevQuad& M, const u16v& head, f3 o, f3 d, uint64_t& 
 RTP_DEV u16v head_at(const DevQuad* q) { return *reinterpret_cast<const u16v*>(q); }
 template <int K>
 RTP_DEV void scan_kind_pf(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d, uint64_t& best, u16v& cur) {
-#if RTP_SCAN_PP && RTP_SCAN_PTR
   // (the prefetches read at most two records past quads[] -- still inside
   // DevScene, whose spheres[] follow -- and those values are never used)
   const DevQuad* qp = sc->quads + b;
@@ -155,49 +102,7 @@ RTP_DEV void scan_kind_pf(const DevScene* __restrict__ sc, int b, int e, f3 o, f
     cur = head_at(qp + 2);
     scan_one<K>(qp[1], nxt, o, d, best);
   }
-  return;
-#elif RTP_SCAN_PP
-  for (int q = b; q < e; q += 2) {
-    const u16v nxt = quad_head(sc, q + 1);
-    scan_one<K>(sc->quads[q], cur, o, d, best);
-    if (q + 1 >= e) {
-      cur = nxt;
-      break;
-    }
-    cur = quad_head(sc, q + 2);
-    scan_one<K>(sc->quads[q + 1], nxt, o, d, best);
-  }
-  return;
-#endif
-  for (int q = b; q < e; q++) {
-    const u16v nxt = quad_head(sc, q + 1);
-    QuadGeom G;
-    __builtin_memcpy(&G, &cur, sizeof(G));
-    float t;
-    const bool ok = quad_hit_masked<K>(G, sc->quads[q], o, d, t);
-    const uint64_t key = (uint64_t)__float_as_uint(t) << 32 | G.key_lo;
-    best = (ok && t > 0.001f && key < best) ? key : best;
-    cur = nxt;
-  }
 }
-#else
-template <int K>
-RTP_DEV void scan_kind(const DevScene* __restrict__ sc, int g, f3 o, f3 d, Hit& h, int& best) {
-  const int b = sc->kind_begin[g], e = sc->kind_begin[g + 1];
-  for (int q = b; q < e; q++) {
-    const DevQuad& Q = sc->quads[q];
-    float t;
-    const bool ok = quad_hit_masked<K>(Q, Q, o, d, t);
-    const int orig = Q.orig;
-    if (ok && t > 0.001f && (t < h.t || (t == h.t && orig < best))) {
-      h.t = t;
-      h.kind = 0;
-      h.idx = q;
-      best = orig;
-    }
-  }
-}
-#endif
 
 // SphereLeafIntersector::hit's accepted root without the tmax test: the
 // reference takes r1 = (-b-sq)/a if tmin < r1 < tmax, else r2 = (-b+sq)/a if
@@ -223,10 +128,8 @@ RTP_DEV bool sphere_root(f3 o, f3 d, float tmin, f3 c, float rr, float& t_out) {
 // lexicographic minimum of (t, quads before spheres, sphere index); the walk
 // visits spheres in BVH order and keeps that minimum explicitly.  Node boxes
 // only cull (padded on the host; compared with slack here), so no sphere
-// whose root could win is skipped.
-#ifndef RTP_BVH_PREFETCH
-#define RTP_BVH_PREFETCH 0  // 1: load node i+1 while testing i (was faster with flat loads; 16% slower with global ones)
-#endif
+// whose root could win is skipped.  (Loading node i+1 while testing i was
+// faster with flat loads and 16% slower with global ones: DESIGN.md 4.1.)
 RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
   const float tmin = 0.001f;
   const float ix = __builtin_amdgcn_rcpf(fabsf(d.x) < 1e-20f ? copysignf(1e-20f, d.x) : d.x);
@@ -259,17 +162,6 @@ RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
   float4 a = nodes[0], b = nodes[1];
   while (ni < nn) {
     const int skip = __float_as_int(a.w), leaf = __float_as_int(b.w);
-#if RTP_BVH_PREFETCH
-    // node ni+1 (the near child when ni is entered) is loaded while ni is
-    // tested; with RTP_BVH_PREFETCH=2 the skip target too, so either way the
-    // next node is already in flight
-    const int nx = min(ni + 1, nn - 1);
-    const float4 an = nodes[2 * nx], bn = nodes[2 * nx + 1];
-#if RTP_BVH_PREFETCH >= 2
-    const int sx = min(skip, nn - 1);
-    const float4 as = nodes[2 * sx], bs = nodes[2 * sx + 1];
-#endif
-#endif
     int next;
     if (leaf == kBvhLeafSphere) {  // one embedded sphere: a.xyz centre, b.x radius^2, b.y index
       float t;
@@ -293,23 +185,10 @@ RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
       }
       next = (hit && !leaf) ? ni + 1 : skip;
     }
-#if RTP_BVH_PREFETCH >= 2
-    a = (next == ni + 1) ? an : as;
-    b = (next == ni + 1) ? bn : bs;
-#elif RTP_BVH_PREFETCH
-    if (next == ni + 1) {
-      a = an;
-      b = bn;
-    } else if (next < nn) {
-      a = nodes[2 * next];
-      b = nodes[2 * next + 1];
-    }
-#else
     if (next < nn) {
       a = nodes[2 * next];
       b = nodes[2 * next + 1];
     }
-#endif
     ni = next;
   }
 }
@@ -344,21 +223,12 @@ RTP_DEV void fill_qshade(const DevScene* __restrict__ sc, float* s_qshade) {
 // two smallest lower bounds, runs the exact test on the first (quad_hit_axis
 // on the quad's PreExact record, a per-lane load from the small global prex
 // table: the kind's own parallelogram arithmetic in the quad's axes, bit-equal
-// to it; with RTP_PRE_AXIS_EXACT=0 the generic kind-0 test on its DevQuad,
-// equal because the skipped terms are exact zeros), and is done when the
-// second lower bound exceeds the best exact hit: every other candidate's
-// exact t is larger, so it loses whatever its index.  Otherwise -- near an
-// edge, a near tie, no finite ray, coordinates beyond kPreLim -- the lane
-// runs the exact scan of every axis-plane quad, as without the prefilter.
-#ifndef RTP_PREFILTER
-#define RTP_PREFILTER 1
-#endif
-#ifndef RTP_PRE_ASM
-#define RTP_PRE_ASM 1  // v_and_or_b32 / v_med3_u32 in the prefilter loop (the compiler emits 2 + 2 ops)
-#endif
-#ifndef RTP_LDS_PAD
-#define RTP_LDS_PAD 0  // (experiments) extra bytes of pool LDS per block
-#endif
+// to it), and is done when the second lower bound exceeds the best exact hit:
+// every other candidate's exact t is larger, so it loses whatever its index.
+// Otherwise -- near an edge, a near tie, no finite ray, coordinates beyond
+// kPreLim -- the lane runs the exact scan of every axis-plane quad, as
+// without the prefilter.  (The host disables the prefilter for scenes it
+// does not cover, and with RTP_PREFILTER=0: DevScene::n_pre == 0.)
 constexpr float kPreTmin = 0.0005f;  // candidates: approximate t above this (accepted hits: t > 0.001)
 constexpr float kPreLimD = 16.0f;    // larger |o| or |d| components: exact scan (margin bound below tmin)
 constexpr float kPreK = 0x1p-18f;    // margin factor, 64 units of 2^-24
@@ -371,12 +241,11 @@ RTP_DEV float comp(f3 v) {
 // k1 <= k2: the two smallest candidate keys {bits(t - m) & ~31, quad position}
 // (positive floats order like their bit patterns; rounding the low bits
 // down keeps the lower bound).  No candidate: ~0u.
-// RTP_PRE_PF: each PreQuad as one s_load_dwordx8, the next one's issued
-// before the current one is tested (as scan_kind_pf); `cur` carries quad b's
-// record in and quad e's (the next axis group's first) out.
-#ifndef RTP_PRE_PF
-#define RTP_PRE_PF 1
-#endif
+// Each PreQuad is one s_load_dwordx8, the next one's issued before the
+// current one is tested (as scan_kind_pf); `cur` carries quad b's record in
+// and quad e's (the next axis group's first) out.  v_and_or_b32 / v_med3_u32
+// are inline asm: the compiler emits 2 + 2 ops for them, which left the
+// prefilter at break-even.
 typedef uint32_t u8v __attribute__((ext_vector_type(8)));
 RTP_DEV u8v pre_rec(const DevScene* __restrict__ sc, int i) {
   return reinterpret_cast<const u8v*>(sc->pre)[min(i, kMaxPre - 1)];
@@ -399,23 +268,14 @@ RTP_DEV void pre_axis(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d,
     // t = +-inf (d[A] ~ 0) gives NaN or inf here and at worst a key above
     // every finite one; the exact test rejects such a quad (|det| < eps)
     const bool ok = (fmaxf(ub, uc) <= m) & (t > kPreTmin);
-#if RTP_PRE_ASM
     uint32_t key;
     asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(key) : "v"(__float_as_uint(t - m)), "v"(~31u), "s"((uint32_t)P.qpos));
     return ok ? key : ~0u;
-#else
-    return ok ? ((__float_as_uint(t - m) & ~31u) | (uint32_t)P.qpos) : ~0u;
-#endif
   };
   auto fold = [&](uint32_t key) {  // keep the two smallest keys
-#if RTP_PRE_ASM
     asm("v_med3_u32 %0, %1, %2, %3" : "=v"(k2) : "v"(k1), "v"(k2), "v"(key));
-#else
-    k2 = min(k2, max(k1, key));
-#endif
     k1 = min(k1, key);
   };
-#if RTP_PRE_PF && RTP_SCAN_PTR
   // ping-pong heads, pointer walk (as scan_kind_pf; prefetches past pre[]
   // stay inside DevScene: prex[] follows)
   auto as_pre = [](const u8v& v) {
@@ -434,35 +294,11 @@ RTP_DEV void pre_axis(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d,
     cur = *reinterpret_cast<const u8v*>(pq + 2);
     fold(key_of(as_pre(nxt)));
   }
-#else
-  for (int i = b; i < e; i++) {
-#if RTP_PRE_PF
-    const u8v nxt = pre_rec(sc, i + 1);
-    PreQuad P;
-    __builtin_memcpy(&P, &cur, sizeof(P));
-#else
-    const PreQuad& P = sc->pre[i];
-#endif
-    fold(key_of(P));
-#if RTP_PRE_PF
-    cur = nxt;
-#endif
-  }
-#endif
 }
 
 // quad_hit_masked<K>'s parallelogram path for an axis-plane quad of any of
 // the kinds 1..6, the kind chosen per lane: the same products, sums and
 // signs (derived in DESIGN.md 4.1), on o and d permuted into the quad's axes.
-#ifndef RTP_PRE_AXIS_EXACT
-#define RTP_PRE_AXIS_EXACT 1
-#endif
-#ifndef RTP_PREX_WIDE
-#define RTP_PREX_WIDE 1  // the candidate's PreExact as four 16-byte loads issued together
-#endif
-#ifndef RTP_PREX_EARLY
-#define RTP_PREX_EARLY 0  // 1: ... issued before the exact scan of kinds 7..10, 0 (which hides their latency)
-#endif
 RTP_DEV bool quad_hit_axis(const PreExact& E, f3 o, f3 d, float& t_out) {
   const bool x0 = E.i == 0, x1 = E.i == 1, pos = E.s > 0;
   auto perm = [&](f3 v, float& vi, float& va, float& vj) {
@@ -488,11 +324,7 @@ RTP_DEV bool quad_hit_axis(const PreExact& E, f3 o, f3 d, float& t_out) {
   const f2v Qa = -(Tj * E.bs);                    // -s * T_j b
   const f2v be2 = (f2v{dj, dj} * Qj + f2v{da, da} * Qa) * inv_det;  // (beta, -bp)
   const float t = (E.c * Qj.x) * inv_det;
-#if RTP_MIN3_ACCEPT
   const bool ok1 = !(fabsf(det) < kEps) & !(fminf(fminf(al2.x, be2.x), t) < 0.0f);  // (see quad_hit_masked)
-#else
-  const bool ok1 = !(fabsf(det) < kEps) & !(al2.x < 0.0f) & !(be2.x < 0.0f) & !(t < 0.0f);
-#endif
   const bool second = (al2.x + be2.x) > 1.0f;
   const bool bad2 = (al2.y > 0.0f) | (be2.y > 0.0f);
   t_out = t;
@@ -503,40 +335,12 @@ template <bool kBvh>
 RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefilter = false,
                         uint32_t* full_out = nullptr) {
   Hit h{3.40282347e+38f, -1, 0};
-  int best = 0x7fffffff;
   const float tmin = 0.001f;
-#if RTP_DUP >= 11 && RTP_DUP <= 14
-  {  // cost attribution of the closest-hit parts (see RTP_DUP)
-    Hit h2 = h;
-#if RTP_HIT_KEY
-    uint64_t b2 = kNoHitKey;
-#define RTP_SCAN2(K, G) scan_kind<K>(sc, G, o2, d, b2)
-#else
-    int b2 = best;
-#define RTP_SCAN2(K, G) scan_kind<K>(sc, G, o2, d, h2, b2)
-#endif
-    f3 o2 = o;
-    RTP_OPQ(o2.x);
-    if (RTP_DUP == 11) {
-      RTP_SCAN2(1, 0); RTP_SCAN2(2, 1); RTP_SCAN2(3, 2); RTP_SCAN2(4, 3); RTP_SCAN2(5, 4); RTP_SCAN2(6, 5);
-    } else if (RTP_DUP == 12) {
-      RTP_SCAN2(7, 6); RTP_SCAN2(8, 7); RTP_SCAN2(9, 8);
-    } else if (RTP_DUP == 13) {
-      RTP_SCAN2(0, 10);
-    } else {
-      float t;
-      if (sphere_hit(o2, d, tmin, h2.t, ld3(sc->spheres[0].c), sc->spheres[0].rr, t)) h2.t = t;
-    }
-    if (__float_as_uint(h2.t) == 0x7fc12345u || (uint32_t)b2 == 0x12345u) h.idx ^= 1;
-#undef RTP_SCAN2
-  }
-#endif
   // the (t, orig) key minimum: the order the kinds are scanned in is free
-#if RTP_HIT_KEY
   uint64_t key = kNoHitKey;
-  // kinds 7..10 and 0: the exact scan, always (their keys are final)
-  auto scan_rest = [&]() {
-#if RTP_SCAN_PF
+  bool full = true;  // this lane needs the exact scan of the axis-plane quads (kinds 1..6)
+  const bool pre = prefilter && sc->n_pre > 0;  // wave-uniform
+  {  // kinds 7..10 and 0: the exact scan, always (their keys are final)
     const int g6 = sc->kind_begin[6], g7 = sc->kind_begin[7], g8 = sc->kind_begin[8], g9 = sc->kind_begin[9],
               g10 = sc->kind_begin[10], g11 = sc->kind_begin[11];
     u16v cur = quad_head(sc, g6);
@@ -545,36 +349,7 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
     scan_kind_pf<9>(sc, g8, g9, o, d, key, cur);
     scan_kind_pf<10>(sc, g9, g10, o, d, key, cur);
     scan_kind_pf<0>(sc, g10, g11, o, d, key, cur);
-#else
-    scan_kind<7>(sc, 6, o, d, key);
-    scan_kind<8>(sc, 7, o, d, key);
-    scan_kind<9>(sc, 8, o, d, key);
-    scan_kind<10>(sc, 9, o, d, key);
-    scan_kind<0>(sc, 10, o, d, key);
-#endif
-  };
-  bool full = true;  // this lane needs the exact scan of the axis-plane quads (kinds 1..6)
-#if RTP_DUP == 15
-  {  // cost attribution: the exact scan of kinds 7..10 and 0 once more, on an opaque origin
-    f3 o2 = o;
-    RTP_OPQ(o2.x);
-    uint64_t k2 = kNoHitKey;
-    const int g6 = sc->kind_begin[6], g7 = sc->kind_begin[7], g8 = sc->kind_begin[8], g9 = sc->kind_begin[9],
-              g10 = sc->kind_begin[10], g11 = sc->kind_begin[11];
-    u16v cur = quad_head(sc, g6);
-    scan_kind_pf<7>(sc, g6, g7, o2, d, k2, cur);
-    scan_kind_pf<8>(sc, g7, g8, o2, d, k2, cur);
-    scan_kind_pf<9>(sc, g8, g9, o2, d, k2, cur);
-    scan_kind_pf<10>(sc, g9, g10, o2, d, k2, cur);
-    scan_kind_pf<0>(sc, g10, g11, o2, d, k2, cur);
-    if ((uint32_t)k2 == 0x12345u) key ^= 1;
   }
-#endif
-#if RTP_PREFILTER
-  const bool pre = prefilter && sc->n_pre > 0;  // wave-uniform
-#if !RTP_PREX_EARLY
-  scan_rest();
-#endif
   if (pre) {
     const bool lane_ok = (int)(fabsf(o.x) <= kPreLimD) & (int)(fabsf(o.y) <= kPreLimD) &
                          (int)(fabsf(o.z) <= kPreLimD) & (int)(fabsf(d.x) <= kPreLimD) &
@@ -584,65 +359,31 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
     const float ma = kPreK * dmax, mb = kPreK * (omax + (sc->pre_scale + 1.0f));
     uint32_t k1 = ~0u, k2 = ~0u;
     const int p0 = sc->pre_begin[0], p1 = sc->pre_begin[1], p2 = sc->pre_begin[2], p3 = sc->pre_begin[3];
-    u8v pcur = RTP_PRE_PF ? pre_rec(sc, p0) : u8v{};
+    u8v pcur = pre_rec(sc, p0);
     pre_axis<0>(sc, p0, p1, o, d, ma, mb, k1, k2, pcur);
     pre_axis<1>(sc, p1, p2, o, d, ma, mb, k1, k2, pcur);
     pre_axis<2>(sc, p2, p3, o, d, ma, mb, k1, k2, pcur);
-#if RTP_PRE_AXIS_EXACT && RTP_PREX_WIDE
     // the candidate's PreExact record: four 16-byte per-lane loads issued
-    // together (every lane: k1 = ~0u reads record 31, in bounds, unused),
-    // with RTP_PREX_EARLY before the exact scan of kinds 7..10 and 0, whose
-    // VALU work then hides their latency (field-wise they compiled to ~4
-    // dependent load / s_waitcnt vmcnt round trips)
+    // together (every lane: k1 = ~0u reads record 31, in bounds, unused);
+    // field-wise they compiled to ~4 dependent load / s_waitcnt vmcnt round
+    // trips.  (Issuing them before the exact scan above ran out of VGPRs.)
     typedef float f4v __attribute__((ext_vector_type(4)));
     const auto* gx = (const __attribute__((address_space(1))) f4v*)(sc->prex) + 4 * (k1 & 31u);
     f4v xr[4] = {gx[0], gx[1], gx[2], gx[3]};
     static_assert(sizeof(PreExact) == sizeof(xr), "PreExact is four 16-byte loads");
-#if RTP_PREX_EARLY
-    scan_rest();
-#endif
     if (lane_ok && k1 != ~0u) {  // (finite o, d: the generic arithmetic equals the kind's)
       PreExact Q;
       __builtin_memcpy(&Q, xr, sizeof(Q));
       float t;
       const bool ok = quad_hit_axis(Q, o, d, t);
-#else
-#if RTP_PREX_EARLY
-    scan_rest();
-#endif
-    if (lane_ok && k1 != ~0u) {  // (finite o, d: the generic arithmetic equals the kind's)
-#if RTP_PRE_AXIS_EXACT
-      const auto* gx = (const __attribute__((address_space(1))) PreExact*)(sc->prex);
-      const PreExact& Q = *(const PreExact*)(gx + (k1 & 31u));  // a per-lane (global) load
-      float t;
-      const bool ok = quad_hit_axis(Q, o, d, t);
-#else
-      // a per-lane load: measured faster than an LDS copy.  Through a global
-      // (address space 1) pointer: the generic one compiled to flat loads.
-      const auto* gq = (const __attribute__((address_space(1))) DevQuad*)(sc->quads);
-      const DevQuad& Q = *(const DevQuad*)(gq + (k1 & 31u));
-      float t;
-      const bool ok = quad_hit_masked<0>(Q, Q, o, d, t);
-#endif
-#endif
       const uint64_t kq = (uint64_t)__float_as_uint(t) << 32 | Q.key_lo;
       key = (ok && t > 0.001f && kq < key) ? kq : key;
     }
     full = !lane_ok || (k2 & ~31u) <= (uint32_t)(key >> 32);  // k2 = ~0u (none) never is
   }
-#if RTP_PREX_EARLY
-  else {
-    scan_rest();
-  }
-#endif
   if (full_out) *full_out = !pre ? 2u : full ? 1u : 0u;  // 2: prefilter off for this scene
-#else
-  scan_rest();
-  if (full_out) *full_out = 2u;
-#endif
   if (__ballot(full)) {
     if (full) {
-#if RTP_SCAN_PF
       const int g0 = sc->kind_begin[0], g1 = sc->kind_begin[1], g2 = sc->kind_begin[2], g3 = sc->kind_begin[3],
                 g4 = sc->kind_begin[4], g5 = sc->kind_begin[5], g6 = sc->kind_begin[6];
       u16v cur = quad_head(sc, g0);
@@ -652,35 +393,13 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
       scan_kind_pf<4>(sc, g3, g4, o, d, key, cur);
       scan_kind_pf<5>(sc, g4, g5, o, d, key, cur);
       scan_kind_pf<6>(sc, g5, g6, o, d, key, cur);
-#else
-      scan_kind<1>(sc, 0, o, d, key);
-      scan_kind<2>(sc, 1, o, d, key);
-      scan_kind<3>(sc, 2, o, d, key);
-      scan_kind<4>(sc, 3, o, d, key);
-      scan_kind<5>(sc, 4, o, d, key);
-      scan_kind<6>(sc, 5, o, d, key);
-#endif
     }
   }
-  (void)best;
   if (key != kNoHitKey) {
     h.t = __uint_as_float((uint32_t)(key >> 32));
     h.kind = 0;
     h.idx = (int)(key & 0xffu);
   }
-#else
-  scan_kind<1>(sc, 0, o, d, h, best);
-  scan_kind<2>(sc, 1, o, d, h, best);
-  scan_kind<3>(sc, 2, o, d, h, best);
-  scan_kind<4>(sc, 3, o, d, h, best);
-  scan_kind<5>(sc, 4, o, d, h, best);
-  scan_kind<6>(sc, 5, o, d, h, best);
-  scan_kind<7>(sc, 6, o, d, h, best);
-  scan_kind<8>(sc, 7, o, d, h, best);
-  scan_kind<9>(sc, 8, o, d, h, best);
-  scan_kind<10>(sc, 9, o, d, h, best);
-  scan_kind<0>(sc, 10, o, d, h, best);
-#endif
   static_assert(kQuadKinds == 11, "closest_hit scans every kind");
   if constexpr (kBvh) {
     spheres_bvh(sc, o, d, h);
@@ -748,14 +467,6 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
     dbg[kDbgFallbackSteps] += m ? 1 : 0;
     dbg[kDbgFallbackLanes] += (unsigned long long)__popcll(m);
   }
-#if RTP_DUP == 1
-  {
-    f3 o2 = org;
-    RTP_OPQ(o2.x);
-    const Hit h2 = closest_hit<kBvh>(sc, o2, dir);
-    RTP_SINK(h2.t, seed);
-  }
-#endif
   if (st) {
     const unsigned long long t1s = __builtin_amdgcn_s_memtime();
     dbg[kDbgCyclesIntersect] += t1s - t0;
@@ -804,7 +515,6 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
     float sph_ctm = -1.0f;  // sqrt(1 - R^2/|c-hp|^2) when the generator made it (sphere_pdf_value reuses it)
     uint32_t tw = wang(seed);  // which (PdfWorklet.h:20)
     seed = tw;
-#if RTP_MERGED_GEN
     // The three generators as one branch-free pass.  Cosine (PdfWorklet.h:
     // 63-79) and light-sphere (:193-213) directions share the ONB, the
     // sincos of phi = 2*pi*r1 and local(); they differ in w, in which draw
@@ -830,50 +540,12 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
     // x = cos(phi)*sqrt(1-z*z) (and (c*1)*s == c*s exactly)
     const float dist2 = dot(direction, direction);
     const float q = sqrt_exact(is_cos ? 1 - r2 : 1 - L.srr / dist2);
-#if RTP_REUSE_CTM
     sph_ctm = is_cos ? -1.0f : q;
-#endif
     const float z = is_cos ? q : 1 + r2 * (q - 1);
     const float rad = sqrt_exact(is_cos ? r2 : 1 - z * z);
     const float m = is_cos ? 2.0f : 1.0f;
     const f3 gcs = de_nan(local(guvw, mk(cphi * m * rad, sphi * m * rad, z)));
-#if RTP_DUP == 4
-    {
-      f3 w2 = wdir;
-      float r1b = r1;
-      RTP_OPQ(w2.x);
-      RTP_OPQ(r1b);
-      const Onb u2 = build_from_w(w2);
-      float s2, c2;
-      rtp_sincosf((float)(2 * kPi * r1b), &s2, &c2);
-      const float q2 = sqrt_exact(is_cos ? 1 - r2 : 1 - L.srr / dist2);
-      const float rad2 = sqrt_exact(is_cos ? r2 : 1 - q2 * q2);
-      const f3 g2 = de_nan(local(u2, mk(c2 * m * rad2, s2 * m * rad2, q2)));
-      RTP_SINK(g2.x, seed);
-    }
-#endif
     gen = is_quad ? genq : gcs;
-#else
-    if (tw < t1) {  // cosine (PdfWorklet.h:63-79)
-      float r1 = randf(seed);
-      float r2 = randf(seed);
-      Onb uvw = build_from_w(hn);
-      gen = de_nan(local(uvw, random_cosine_direction(r1, r2)));
-    } else if (tw < t2) {  // light quad (PdfWorklet.h:112-137)
-      float r1 = randf(seed);
-      float r2 = randf(seed);
-      float r3 = randf(seed);
-      f3 rp = mk(L.gx0 + r1 * L.gdx, L.gy0 + r2 * L.gdy, L.gz0 + r3 * L.gdz);
-      gen = sub(rp, hp);
-    } else {  // light sphere (PdfWorklet.h:193-213); g++ evaluates the draws right to left
-      float first = randf(seed);
-      float second = randf(seed);
-      f3 direction = sub(ld3(L.sc), hp);
-      float dist2 = dot(direction, direction);
-      Onb uvw = build_from_w(direction);
-      gen = de_nan(local(uvw, random_to_sphere(L.srr, dist2, second, first)));
-    }
-#endif
     // applyPDFs: QuadPDFWorklet, SpherePDFWorklet (1 discarded draw)
     const float weight = 0.5f;
     float sum = 0;
@@ -882,14 +554,6 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
     sum += weight * quad_pdf_value(L, hp, gen, rg);
     (void)randf(seed);
     sum += weight * sphere_pdf_value(L, hp, gen, sph_ctm);
-#if RTP_DUP == 2 || RTP_DUP == 3
-    {
-      f3 h2 = hp;
-      RTP_OPQ(h2.x);
-      const float v2 = RTP_DUP == 2 ? quad_pdf_value(L, h2, gen, rmag(gen)) : sphere_pdf_value(L, h2, gen);
-      RTP_SINK(v2, seed);
-    }
-#endif
     // PDFCosineWorklet (ScatterWorklet.h:96-112): mixture in double
     const f3 ug = scl(gen, rg);       // unit_vector(gen)
     const f3 w_hn = unit_vector(hn);  // build_from_w(hn).w (u and v are unused here)
@@ -905,20 +569,6 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
       sp = (cosine < 0) ? 0.f : cos_over_pi(cosine);
     }
     double sctr = (double)sp / pdf_val;
-#if RTP_DUP == 5
-    {
-      f3 g2 = gen;
-      RTP_OPQ(g2.x);
-      const Onb u2 = build_from_w(hn);
-      const float cs1 = dot(unit_vector(g2), u2.w);
-      const float cv2 = (cs1 > 0) ? cos_over_pi(cs1) : 0.f;
-      const double pv2 = 0.5 * (double)sum + 0.5 * (double)cv2;
-      const float cs2 = dot(hn, unit_vector(g2));
-      const float sp2 = (cs2 < 0) ? 0.f : cos_over_pi(cs2);
-      const double sc2 = (double)sp2 / pv2;
-      RTP_SINK((float)(alb.x * sc2), seed);
-    }
-#endif
     atten = mk((float)(alb.x * sctr), (float)(alb.y * sctr), (float)(alb.z * sctr));
     ps.org = hp;
     ps.dir = gen;
@@ -971,9 +621,6 @@ RTP_DEV int64_t tile_pixel(const KP& p, int k) {
 // is below 2^24 (the estimate is then off by at most one), else by integer
 // division (a wave-uniform branch).  The compiler's signed % and / cost ~40
 // VALU per refill.
-#ifndef RTP_PIXEL_XY
-#define RTP_PIXEL_XY 1
-#endif
 template <bool kTiles = false, class KP>
 RTP_DEV void pixel_xy(const KP& p, int k, int& pi, int& pj) {
   if constexpr (kTiles) {
@@ -1111,10 +758,13 @@ RTP_DEV void set_priority(float lag) {  // s_setprio needs an immediate
 #ifndef RTP_POOL_MAX_VGPR
 #define RTP_POOL_MAX_VGPR 96
 #endif
-// byte offset of the KParams argument in rtp_render_pool's kernarg segment
-// (after the 8-byte scene pointer; checked against the code object's
-// argument metadata by tests/test_abi.py)
-constexpr int kKParamsOffset = 8;
+// byte offset of the KParams argument in rtp_render_pool's kernarg segment:
+// the first argument (the scene pointer) rounded up to KParams' alignment
+// (also checked against the code object's argument metadata by
+// tests/test_abi.py)
+constexpr int kKParamsOffset =
+    (int)((sizeof(const DevScene*) + alignof(KParams) - 1) / alignof(KParams) * alignof(KParams));
+static_assert(alignof(KParams) <= 16 && kKParamsOffset == 8, "KParams follows the 8-byte scene pointer");
 typedef const __attribute__((address_space(4))) KParams CKP;
 // The kernel arguments re-read where they are used (scalar loads from the
 // kernarg segment): values loaded once and kept live through the scheduling
@@ -1133,7 +783,7 @@ template <bool kStats, bool kBvh, bool kTiles = false>
 #define RTP_POOL_VGPR_ATTR
 #endif
 __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_ATTR rtp_render_pool(const DevScene* __restrict__ sc, KParams p, int n_waves) {
-  __shared__ __align__(16) unsigned char smem[kPoolLdsBytes + RTP_LDS_PAD];
+  __shared__ __align__(16) unsigned char smem[kPoolLdsBytes];
   __shared__ __align__(16) float s_qshade[kLdsQuads * kQShadeFloats];
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
@@ -1175,7 +825,6 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
   int unfinished = n_slots;                // stats only: pixels with samples still to run
   unsigned long long t_tail = 0;
 
-#if RTP_DEFER_RADIANCE
   // attenuation history per pixel SLOT, [d][wave*kPool + slot], D rows: a
   // pixel has one sample in flight, so its history survives until the
   // fast-forward batch that computes the sample's radiance (row k of a
@@ -1183,10 +832,6 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
   float4* __restrict__ const hist_base = reinterpret_cast<float4*>(p.hist) + (int64_t)w * kPool;
   const int64_t stride = (int64_t)n_waves * kPool;
   float4* __restrict__ hist = hist_base;  // per lane: hist_base + slot of its path
-#else
-  float4* __restrict__ hist = reinterpret_cast<float4*>(p.hist) + ((int64_t)w * 64 + lane);  // [d][lane]
-  const int64_t stride = (int64_t)n_waves * 64;
-#endif
   const f3 eye = ld3(p.cam.eye);
 
   // diagnostics (uniform branch on a kernel argument; off in production)
@@ -1231,7 +876,6 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
         fseed = s_seed[fslot];
         frem = s_rem[fslot];
       }
-#if RTP_FF_EARLY
       // the first jump-table read is issued before the radiance loads below,
       // so its latency overlaps theirs: the direct table of the sample's
       // remaining count when there is one (then it is the only read), else
@@ -1245,8 +889,6 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
         GU32* src = (GU32*)(has_direct ? FP.ffd + ((uint64_t)(frc - FP.ffd_first) << 32) : FP.ff[0]);
         early = src[fseed];
       }
-#endif
-#if RTP_DEFER_RADIANCE
       if (mine) {
         // back-to-front radiance of the pixel's finished sample (path_radiance),
         // banked in sample order before the pixel's next sample can start
@@ -1258,7 +900,6 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
           const float4* __restrict__ hp = hist_base + fslot;
           const float4 e = hp[(int64_t)k_end * stride];
           float sx = e.x + 0.0f, sy = e.y + 0.0f, sz = e.z + 0.0f;
-#if RTP_FF_EARLY
           // two history rows per trip, both loads in flight together; the
           // products stay in the reference's order (depth k_end-1 down to 0)
           int dd = k_end - 1;
@@ -1277,14 +918,6 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
             sy = 0.0f + a.y * sy;
             sz = 0.0f + a.z * sz;
           }
-#else
-          for (int dd = k_end - 1; dd >= 0; dd--) {
-            const float4 a = hp[(int64_t)dd * stride];
-            sx = 0.0f + a.x * sx;
-            sy = 0.0f + a.y * sy;
-            sz = 0.0f + a.z * sz;
-          }
-#endif
           c = mk(sx, sy, sz);
         } else {
           const float v = (flags & kEndNonfinite) ? __builtin_nanf("") : 0.0f;
@@ -1294,11 +927,9 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
         s_g[fslot] = s_g[fslot] + c.y;
         s_b[fslot] = s_b[fslot] + c.z;
       }
-#endif
       // jump over 32 / 16 / 8 / 4 dead depths with one table read each
       // (HBM-resident tables of the dead-step map, built once per device),
       // then hash the few remaining depths
-#if RTP_FF_EARLY
       if (has_direct) {
         fseed = early;
         frem = 0;
@@ -1306,10 +937,8 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
         fseed = early;
         frem -= 32;
       }
-#endif
-      const bool hash_now = mine;
 #pragma unroll
-      for (int j = RTP_FF_EARLY ? 1 : 0; j < kFfTables; j++) {
+      for (int j = 1; j < kFfTables; j++) {
         GU32* __restrict__ tab = (GU32*)kparams().ff[j];
         if (tab != nullptr && mine && frem >= (32 >> j)) {
           fseed = tab[fseed];
@@ -1318,47 +947,28 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
       }
       int iters = 0;
       for (int i = 0;; i++) {
-        const bool act = hash_now && i < frem;
+        const bool act = mine && i < frem;
         if (!__any(act)) break;
         if (act) fseed = dead_step(fseed, t1, t2);
-#if RTP_DUP == 6
-        if (act) {
-          uint32_t f2 = fseed;
-          asm volatile("" : "+v"(f2));
-          f2 = dead_step(f2, t1, t2);
-          if (f2 == 0x12345u) fslot ^= 1;
-        }
-#endif
         iters++;
       }
       bool again = false;
       if (mine) s_seed[fslot] = fseed;
-      if (hash_now) again = s_samples[fslot] < (uint32_t)S;
-      if (want_dbg) unfinished -= __popcll(__ballot(hash_now && !again));
-#if RTP_FAIR_READY
+      if (mine) again = s_samples[fslot] < (uint32_t)S;
+      if (want_dbg) unfinished -= __popcll(__ballot(mine && !again));
       // Fair share: a pixel whose completed samples are at or below the
       // wave's average (ff_tail / n_slots) goes to the FRONT of the READY
       // ring, the others to the back.  FIFO alone let cheap pixels (short
       // paths, back sooner) take more than their share of lanes, so the
       // expensive pixels' sequential sample chains ran on alone at the end
       // (17% of bounce steps with ~12 of 64 lanes live).
-#if RTP_URGENT_PERMILLE == 0
       // (samples * n_slots <= 2^23 * 2^8 and ff_tail <= n_slots * spp: 32 bits suffice)
       const bool urgent = again && s_samples[fslot] * (uint32_t)n_slots <= (uint32_t)ff_tail;
-#else
-      const bool urgent = again && (uint64_t)s_samples[fslot] * (uint64_t)n_slots * 1000u <=
-                                       (uint64_t)ff_tail * (uint64_t)(1000 + RTP_URGENT_PERMILLE);
-#endif
       const uint64_t pu = __ballot(urgent), pn = __ballot(again && !urgent);
       ready_head -= __popcll(pu);
       if (urgent) q_ready[(ready_head + (int)lane_rank(pu)) & (kPool - 1)] = (uint16_t)fslot;
       if (again && !urgent) q_ready[(ready_tail + (int)lane_rank(pn)) & (kPool - 1)] = (uint16_t)fslot;
       ready_tail += __popcll(pn);
-#else
-      const uint64_t push = __ballot(again);
-      if (again) q_ready[(ready_tail + (int)lane_rank(push)) & (kPool - 1)] = (uint16_t)fslot;
-      ready_tail += __popcll(push);
-#endif
       ff_head += n;
       wave_sync();
       if (want_dbg) {
@@ -1367,12 +977,9 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
         dbg[kDbgFfIters] += (unsigned long long)iters;
         dbg[kDbgCyclesFf] += __builtin_amdgcn_s_memtime() - t0;
       }
-#if !RTP_FF_FALL
-      continue;
-#endif
-      // (RTP_FF_FALL: on into the refill, which takes the pixels this batch
-      // made READY, and the bounce: a sample's chain spends no iteration of
-      // its own on the fast-forward)
+      // on into the refill, which takes the pixels this batch made READY,
+      // and the bounce: a sample's chain spends no iteration of its own on
+      // the fast-forward
     }
     // ---- refill idle lanes with the next sample of READY pixels ----
     const unsigned long long tb = stamp(want_dbg);
@@ -1382,35 +989,16 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
       if (r < take) {
         slot = q_ready[(ready_head + r) & (kPool - 1)];
         seed = s_seed[slot];
-#if RTP_DEFER_RADIANCE
         hist = hist_base + slot;
-#endif
-#if RTP_CAM_RELOAD
         // the camera and tile constants re-read from the kernel arguments
         // here (kparams): kept live through the loop they were SGPRs spilled
         // to VGPR lanes, ~30 v_readlane per refill (through the kernarg
         // segment pointer: &p would copy p to scratch)
         CKP& P = kparams();
-#else
-        const KParams& P = p;
-#endif
-#if RTP_PIXEL_XY
         int pi, pj;
         pixel_xy<kTiles>(P, slot * n_waves + w, pi, pj);  // (32-bit index: a 64-bit one spilled)
-#else
-        const int64_t pix = pixel_of<kTiles>(P, slot * n_waves + w);  // (32-bit: a 64-bit index spilled)
-        const int pi = (int32_t)pix % P.nx, pj = (int32_t)pix / P.nx;
-#endif
         ps.dir = camera_ray(P.cam, pi, pj, P.nx, P.ny, seed);
-#if RTP_DUP == 7
-        {
-          uint32_t s2 = seed;
-          asm volatile("" : "+v"(s2));
-          const f3 d2 = camera_ray(p.cam, pi, pj, p.nx, p.ny, s2);
-          RTP_SINK(d2.x, seed);
-        }
-#endif
-        ps.org = RTP_CAM_RELOAD ? ld3(P.cam.eye) : eye;
+        ps.org = ld3(P.cam.eye);
         ps.d = 0;
         ps.nonfinite = false;
         has_path = true;
@@ -1432,20 +1020,12 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
         ps.d++;
       } else {
         const int k_end = ps.d;
-#if RTP_DEFER_RADIANCE
         // the radiance product runs in the fast-forward batch (above)
         if (res == kLight) hist[(int64_t)k_end * stride] = make_float4(emit.x, emit.y, emit.z, 0.f);
         // dead depths left: D-1-k_end, plus depth k_end's own draws when the
         // path died there (bounce<.., true> left them to the fast-forward)
         const int rem = D - 1 - k_end + (res != kAlive ? 1 : 0);
         s_rem[slot] = (uint16_t)(rem | (res == kLight ? kEndLight : 0) | (ps.nonfinite ? kEndNonfinite : 0));
-#else
-        const f3 c = path_radiance(res, k_end, emit, ps.nonfinite, hist, stride);
-        s_r[slot] = s_r[slot] + c.x;  // cols += sumtotl (MapperPathTracer.cxx:350), in sample order
-        s_g[slot] = s_g[slot] + c.y;
-        s_b[slot] = s_b[slot] + c.z;
-        s_rem[slot] = (uint16_t)(D - 1 - k_end + (res != kAlive ? 1 : 0));
-#endif
         s_samples[slot] = s_samples[slot] + 1u;
         s_live[slot] = s_live[slot] + (uint32_t)(k_end + 1);
         s_seed[slot] = seed;
@@ -1655,7 +1235,7 @@ extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int bvh, int* variant_ou
   W = std::max<int64_t>(W, by_pool);
   W = std::max<int64_t>(W, 1);
   if (waves_out) *waves_out = (int)W;
-  return RTP_DEFER_RADIANCE ? W * rtp::kPool : W * 64;
+  return W * rtp::kPool;
 }
 
 extern "C" hipError_t rtp_launch_eval_closest(const rtp::DevScene* scene, const float* rays, uint32_t* out,

@@ -43,6 +43,23 @@ def rmse_normalized(a_sum: np.ndarray, b_sum: np.ndarray, spp: int) -> float:
     return float(np.sqrt(np.mean(d * d)))
 
 
+def load_full_frame(path: str) -> dict:
+    """A whole-frame fixture (tools/make_golden.py full_frame_fixture): the
+    rgb sums float32 [N, 3] rebuilt from their four byte planes, the NaN
+    pixel list and the digests of the final seeds and live-bounce counts."""
+    z = np.load(path, allow_pickle=False)
+    g = {k: z[k] for k in z.files}
+    planes = g.pop("rgb_planes")
+    g["rgb"] = np.ascontiguousarray(planes.T).view(np.float32).reshape(-1, 3)
+    return g
+
+
+def sha256_u32(a) -> bytes:
+    import hashlib
+
+    return hashlib.sha256(np.ascontiguousarray(a, dtype="<u4").tobytes()).digest()
+
+
 def set_scene_from_oracle(device, sc) -> None:
     """Upload an oracle Scene (e.g. an edited cornell_box) through rtp_set_scene."""
     nq, ns = sc.n_quads, sc.n_spheres

@@ -10,10 +10,12 @@ import os
 import numpy as np
 import pytest
 
-from _util import assert_render_equal
+from _util import assert_render_equal, load_full_frame, rmse_normalized, same_bits_or_both_nan, sha256_u32
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-RENDERS = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLD, "*.npz")))
+FULL_FRAMES = ["c2_full"]  # whole frames (byte-plane format, tools/make_golden.py full_frame_fixture)
+RENDERS = sorted(n for n in (os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLD, "*.npz")))
+                 if n not in FULL_FRAMES)
 
 
 def _load(name):
@@ -24,6 +26,7 @@ def _load(name):
 def test_fixtures_present():
     assert {"c1_full", "c2_subset", "c3_subset", "c4_subset", "glass_subset", "glass2_subset",
             "c5_shard3_subset"} <= set(RENDERS)
+    assert all(os.path.exists(os.path.join(GOLD, n + ".npz")) for n in FULL_FRAMES)
 
 
 def test_kat_json(oracle):
@@ -82,3 +85,66 @@ def test_hip_reproduces_fixture(device, name):
                                seed_base=int(g["seed_base"]))[:3]
     want = (np.c_[g["rgb"], np.zeros(len(g["pixels"]), np.float32)], g["final_seed"], g["live"])
     assert_render_equal(got, want, name)
+
+
+# ---- the metric's whole frame: C2, 800x800, 1000 spp, depth 50 ----------
+# (BASELINE.json metric "... per-pixel RMSE vs ref": main.cc:253-287, 317-321)
+
+
+def test_c2_full_frame_fixture_is_consistent():
+    g = load_full_frame(os.path.join(GOLD, "c2_full.npz"))
+    nx, ny = int(g["nx"]), int(g["ny"])
+    assert g["rgb"].shape == (nx * ny, 3) and (nx, ny, int(g["spp"]), int(g["depth"])) == (800, 800, 1000, 50)
+    assert np.array_equal(np.flatnonzero(np.isnan(g["rgb"]).any(1)), g["nan_pixels"])
+    assert g["nan_pixels"].size == 670  # NaN pixels of the reference's C2 frame are data
+    # L = live bounces per sample of the whole frame (SURVEY.md 8(d) byte model)
+    assert abs(int(g["live_sum"]) / (nx * ny * 1000) - 3.7066) < 1e-4
+    # the two committed C2 fixtures agree where they overlap (4096 pixels)
+    sub = _load("c2_subset")
+    assert same_bits_or_both_nan(g["rgb"][sub["pixels"]], sub["rgb"]).all()
+
+
+def test_oracle_reproduces_c2_full_frame_rows(oracle):
+    """The checker reproduces a spread of the frame's pixels, NaN pixels included."""
+    g = load_full_frame(os.path.join(GOLD, "c2_full.npz"))
+    rng = np.random.default_rng(5)
+    pix = np.sort(np.r_[rng.choice(g["rgb"].shape[0], 24, replace=False), g["nan_pixels"][:8]]).astype(np.int64)
+    sc = oracle.cornell_box(0)
+    cam = oracle.camera_setup(800, 800)
+    assert np.array_equal(cam.view(np.uint32), g["camera"].view(np.uint32))
+    rgba, _, _ = oracle.render_pixels(sc, cam, 800, 800, 1000, 50, pix)
+    assert same_bits_or_both_nan(rgba[:, :3], g["rgb"][pix]).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["contiguous", "tiles"])
+def test_hip_reproduces_c2_full_frame(device, path):
+    """The whole C2 frame on the GPU -- the bench workload -- bit-exact against
+    the oracle's frame (NaN-aware), final RNG states and live-bounce counts
+    equal (SHA-256 of all 640,000), and the metric's quality gate:
+    per-pixel RMSE of the normalised frame < 1e-4 (it is 0)."""
+    import torch
+
+    import raytracingtherestofyourlife_amd as rtp
+    from raytracingtherestofyourlife_amd import shard
+
+    g = load_full_frame(os.path.join(GOLD, "c2_full.npz"))
+    device.set_cornell_box(0)
+    cam = rtp.default_camera()
+    n = 800 * 800
+    out = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
+    if path == "contiguous":
+        seeds = torch.zeros(n, dtype=torch.int32, device="cuda")
+        live = torch.zeros(n, dtype=torch.int32, device="cuda")
+        device.render_device(cam, 800, 800, 1000, 50, out.data_ptr(), seed_ptr=seeds.data_ptr(),
+                             live_ptr=live.data_ptr(), timed=True)
+        canvas = out.cpu().numpy()
+        assert sha256_u32(seeds.cpu().numpy().view(np.uint32)) == bytes(g["seed_sha256"])
+        assert sha256_u32(live.cpu().numpy().view(np.uint32)) == bytes(g["live_sha256"])
+    else:  # bench.py's instance: the in-kernel 16x16 tile deal, scattered to the canvas
+        device.render_tiles_device(cam, 800, 800, 1000, 50, out.data_ptr(), 0, 1, timed=True)
+        canvas = np.zeros((n, 4), np.float32)
+        canvas[shard.tile_pixels(800, 800, 0, 1)] = out.cpu().numpy()
+    ok = same_bits_or_both_nan(canvas[:, :3], g["rgb"]).all(1)
+    assert ok.all(), f"{int((~ok).sum())} of {n} pixels differ, first {np.flatnonzero(~ok)[:8].tolist()}"
+    assert rmse_normalized(canvas, np.c_[g["rgb"], np.zeros(n, np.float32)], 1000) < 1e-4

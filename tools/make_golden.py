@@ -50,6 +50,33 @@ def render_fixture(name, variant, nx, ny, spp, depth, pixels=None, seed_base=0, 
           f"L={live.sum() / (pixels.size * spp):.4f}, nan_px={int(np.isnan(rgba[:, :3]).any(1).sum())}")
 
 
+def full_frame_fixture(name, variant, nx, ny, spp, depth):
+    """A whole frame at full S x D (the metric's own image, main.cc:253-287,
+    317-321): the un-normalised rgb sums of every pixel, stored as the four
+    byte planes of the float32 bit patterns (deflate packs the exponent planes
+    well); the final seeds and live-bounce counts as SHA-256 digests plus
+    their sums (16 MB of near-random words otherwise)."""
+    if ONLY and name not in ONLY:
+        return
+    import hashlib
+
+    t = time.time()
+    sc = oc.cornell_box(variant)
+    cam = oc.camera_setup(nx, ny)
+    pixels = np.arange(nx * ny, dtype=np.int64)
+    rgba, seeds, live = oc.render_pixels(sc, cam, nx, ny, spp, depth, pixels)
+    rgb = np.ascontiguousarray(rgba[:, :3], dtype=np.float32)
+    planes = rgb.view(np.uint8).reshape(-1, 4).T.copy()  # [byte][value]
+    nan_px = np.flatnonzero(np.isnan(rgb).any(1)).astype(np.int64)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), variant=variant, nx=nx, ny=ny, spp=spp, depth=depth,
+                        camera=cam, rgb_planes=planes, nan_pixels=nan_px,
+                        seed_sha256=np.frombuffer(hashlib.sha256(seeds.astype("<u4").tobytes()).digest(), np.uint8),
+                        live_sha256=np.frombuffer(hashlib.sha256(live.astype("<u4").tobytes()).digest(), np.uint8),
+                        seed_sum=np.uint64(seeds.astype(np.uint64).sum()), live_sum=np.uint64(live.astype(np.uint64).sum()))
+    print(f"{name}: {nx}x{ny} x {spp} spp x depth {depth}: {time.time() - t:.1f}s, "
+          f"L={live.sum() / (pixels.size * spp):.4f}, nan_px={nan_px.size}")
+
+
 def direct_fixture(name, variant, nx, ny, camera=None, clip=(0.1, 5.0)):
     """-direct mode (main.cc:120-251): colour, normals, albedo and depth of
     one camera, full canvas, from the oracle's restatement."""
@@ -109,6 +136,8 @@ def main():
     render_fixture("c1_full", 0, 200, 200, 10, 10)
     # C2 geometry at full spp/depth on a fixed 4096-pixel subset
     render_fixture("c2_subset", 0, 800, 800, 1000, 50, pixels=subset(800 * 800, 4096, 2))
+    # C2, the metric's whole frame (bench.py's workload; ~12 min on 8 cores)
+    full_frame_fixture("c2_full", 0, 800, 800, 1000, 50)
     # C4 geometry (1920x1080, 4096 spp, depth 50) on a 256-pixel subset
     render_fixture("c4_subset", 0, 1920, 1080, 4096, 50, pixels=subset(1920 * 1080, 256, 4))
     # dielectric visible: variant 1 (overlapping, NaN-heavy) and variant 2 (clean)

@@ -13,6 +13,8 @@ ap.add_argument("--depth", type=int, default=50)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--variant", type=int, default=0)
 ap.add_argument("--tiles", action="store_true", help="the tile-deal instance bench.py runs (rank 0 of 1), no live counters")
+ap.add_argument("--world", type=int, default=1, help="--tiles: the deal over this many ranks")
+ap.add_argument("--rank", type=int, default=0, help="--tiles: the rank whose share is rendered")
 ap.add_argument("--list-tiles", action="store_true", help="the pixel-list path over the tile deal's order")
 ap.add_argument("--list-contig", action="store_true", help="the pixel-list path over the contiguous order")
 a = ap.parse_args()
@@ -35,7 +37,8 @@ for r in range(a.reps):
         st = dev.render_device(cam, a.nx, a.ny, a.spp, a.depth, out.data_ptr(), pixel_count=n, pixel_ids_ptr=ids.data_ptr(),
                                stream=s, live_ptr=live.data_ptr(), timed=True)
     elif a.tiles:
-        st = dev.render_tiles_device(cam, a.nx, a.ny, a.spp, a.depth, out.data_ptr(), 0, 1, stream=s, timed=True)
+        st = dev.render_tiles_device(cam, a.nx, a.ny, a.spp, a.depth, out.data_ptr(), a.rank, a.world, stream=s,
+                                     timed=True)
     else:
         st = dev.render_device(cam, a.nx, a.ny, a.spp, a.depth, out.data_ptr(), stream=s, live_ptr=live.data_ptr(),
                                timed=True)
@@ -43,6 +46,7 @@ for r in range(a.reps):
     wall = time.time() - t
     L = live.to(torch.int64).sum().item() / (n * a.spp)
     Lp = (live.to(torch.float64) / a.spp).cpu().numpy()
-    print(json.dumps(dict(rep=r, kernel_ms=st.kernel_ms, wall_s=wall, msamples_per_s=n * a.spp / (st.kernel_ms / 1e3) / 1e6,
+    nr = n // a.world if a.tiles else n
+    print(json.dumps(dict(rep=r, kernel_ms=st.kernel_ms, wall_s=wall, msamples_per_s=nr * a.spp / (st.kernel_ms / 1e3) / 1e6,
                           live_per_sample=L, nan_px=int(torch.isnan(out[:, :3]).any(1).sum().item()),
                           L_pixel_pct={q: round(float(np.percentile(Lp, q)), 3) for q in (50, 90, 99, 99.9, 100)})), flush=True)
