@@ -1,22 +1,29 @@
 """Benchmark of the path-tracing hot path (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak]
 
-One step = one full render of the C2 workload on every rank: Cornell Box,
-800x800 pixels per GPU, 1000 spp, depth 50 (BASELINE.json configs[1]).
-N > 1 (launched by torch.distributed.run, one process per GPU): weak scaling
-by image tiles -- the canvas is 800 x (800*N), 16x16 tiles are dealt to the
-ranks round-robin (every rank renders 640,000 pixels), and the float4
-framebuffer is summed to rank 0 with ONE RCCL reduce per step, overlapped with
-the next step's render (two canvases, alternating; exact: every
-pixel is non-zero on exactly one rank).
+One step = one full render of the C2 workload: Cornell Box 800x800, 1000 spp,
+depth 50 (BASELINE.json configs[1]), the metric's own image.
+N > 1 (launched by torch.distributed.run, one process per GPU):
+  --scaling strong (default): THE 800x800 frame, its 16x16 tiles dealt to the
+      ranks round-robin; each rank renders 1/N of the
+      pixels, and the float4 framebuffer is summed to rank 0 with ONE reduce
+      per step (RCCL over xGMI), overlapped with the next step's render (two
+      canvases, alternating; exact: every pixel is non-zero on one rank).
+  --scaling weak: every rank renders a full 800x800 band of an 800 x 800N
+      canvas (per-GPU work fixed).
 
 Rank 0 prints one JSON line.  `value` = all ranks' samples / max-over-ranks
-wall time of the K timed steps.  `roofline` prices the render kernel with the
-SoA byte model of SURVEY.md 8(d) (56 + 88*L bytes per sample, L = mean live
-bounces per sample, counted by the kernel) against the 8 TB/s HBM peak;
-`cpu_baseline` times the oracle's stage-structured restatement on a bounded
-sample of the same workload on this host (1 thread).
+wall time of the K timed steps (steady state: the renderer's context, scene
+and RNG jump tables are set up before the timed region -- `setup` and
+`first_render_ms` report what that costs, and `one_shot` what a fresh process
+rendering once, like main.cc, would see).  `rmse` / `bit_exact` compare the
+last timed frame (normalised, NormalizeFunctor) with the oracle's committed
+C2 frame (tests/golden/c2_full.npz).  `roofline` prices the render kernel with
+the SoA byte model of SURVEY.md 8(d) (56 + 88*L bytes per sample) against the
+8 TB/s HBM peak; `roofline_valu` gives the VALU-issue bound from the
+committed PMC summary; `cpu_baseline` times the oracle's stage-structured
+restatement on a bounded sample of the same workload on this host.
 """
 from __future__ import annotations
 
@@ -92,15 +99,68 @@ def load_traffic(path: str, cfg: dict):
     return None
 
 
+def load_golden_frame(path: str):
+    """tests/golden/c2_full.npz (tools/make_golden.py full_frame_fixture): the
+    oracle's un-normalised rgb sums [N, 3] and its config, or None."""
+    try:
+        z = np.load(path, allow_pickle=False)
+    except OSError:
+        return None
+    rgb = np.ascontiguousarray(z["rgb_planes"].T).view(np.float32).reshape(-1, 3)
+    return {"rgb": rgb, "nx": int(z["nx"]), "ny": int(z["ny"]), "spp": int(z["spp"]), "depth": int(z["depth"])}
+
+
+def frame_quality(canvas: np.ndarray, gold: dict, spp: int) -> dict:
+    """Per-pixel RMSE of the normalised frames (NormalizeFunctor, main.cc:253-287,
+    before quantisation) and bitwise equality of the sums (NaN-aware)."""
+    import raytracingtherestofyourlife_amd as rtp
+
+    a = np.ascontiguousarray(canvas, dtype=np.float32).copy()
+    b = np.c_[gold["rgb"], np.zeros(len(gold["rgb"]), np.float32)].astype(np.float32)
+    same = (a[:, :3].view(np.uint32) == b[:, :3].view(np.uint32)) | (np.isnan(a[:, :3]) & np.isnan(b[:, :3]))
+    rtp.normalize(a, spp)
+    rtp.normalize(b, spp)
+    d = a[:, :3].astype(np.float64) - b[:, :3].astype(np.float64)
+    return {"rmse": float(np.sqrt(np.mean(d * d))), "bit_exact": bool(same.all()),
+            "pixels_differing": int((~same.all(1)).sum()), "nan_pixels_ref": int(np.isnan(gold["rgb"]).any(1).sum())}
+
+
+def load_valu(path: str, cfg: dict, kernel_ms: float):
+    """VALU-issue bound of the render kernel from a committed PMC summary
+    (tools/pmc_valu.sh): wave64 VALU instructions per launch against the
+    SIMDs' issue capacity at 2 cycles per wave64 instruction
+    (MI355X_MICROARCH.md, per-instruction constants: v_fma_f32 2 cyc on
+    SIMD-32), over the cycles the chip ran (GRBM_GUI_ACTIVE / 8 XCDs).  The
+    live HIP-event kernel time rescales the PMC run's cycles to this run."""
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if not all(t.get(k) == v for k, v in cfg.items()):
+        return None
+    cap = t["simds"] * t["gpu_cycles_per_launch"] / t["cycles_per_wave64_valu"]
+    frac = t["valu_insts_per_launch"] / cap
+    return {"bound": "valu-issue", "achieved": t["valu_insts_per_launch"] / (kernel_ms / 1e3) / 1e12,
+            "peak": t["simds"] * t["clock_ghz"] * 1e9 / t["cycles_per_wave64_valu"] / 1e12,
+            "unit": "T wave64-VALU instr/s", "frac": round(frac, 4),
+            "lanes_per_instr": t.get("lanes_per_instr"), "source": t.get("source")}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong: the one 800x800 frame dealt over the ranks; weak: an 800x800 band per rank")
     ap.add_argument("--nx", type=int, default=800)
-    ap.add_argument("--ny", type=int, default=800, help="rows per GPU (canvas is nx x ny*N)")
+    ap.add_argument("--ny", type=int, default=800, help="rows of the frame (weak: per GPU, canvas nx x ny*N)")
     ap.add_argument("--spp", type=int, default=1000)
     ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--ff-tables", default="on", choices=["on", "auto", "off"],
+                    help="RNG jump-table policy (include/rtp.h rtp_set_ff_tables); on: a long-lived renderer, "
+                         "tables built during setup (reported in `setup`)")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work (0: skip)")
     ap.add_argument("--cpu-budget-mt", type=float, default=6.0, help="seconds of all-cores CPU baseline (0: skip)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -108,6 +168,8 @@ def main() -> None:
     ap.add_argument("--share-gpu", action="store_true", help="every rank uses device 0 (rehearsal on a 1-GPU box)")
     ap.add_argument("--check", action="store_true", help="rank 0 verifies the reduced canvas against a 1-process render")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c2.json"))
+    ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "valu_c2.json"))
+    ap.add_argument("--golden", default=os.path.join(ROOT, "tests", "golden", "c2_full.npz"))
     args = ap.parse_args()
 
     import torch
@@ -129,11 +191,20 @@ def main() -> None:
         else:
             dist.init_process_group("gloo")
 
-    nx, ny = args.nx, args.ny * world
+    strong = args.scaling == "strong"
+    nx, ny = args.nx, args.ny * (1 if strong else world)
     ids_np = shard.tile_pixels(nx, ny, rank, world)
     npix = ids_np.size
+    # setup, timed: the context, the scene, the RNG jump tables (policy), then
+    # the first render -- what a fresh process pays before its first frame
+    torch.cuda.synchronize()
+    t_setup = time.perf_counter()
     dev = rtp.Device(gpu)
+    t_ctx = time.perf_counter()
     dev.set_cornell_box(0)
+    t_scene = time.perf_counter()
+    ff = dev.set_ff_tables(args.ff_tables)
+    t_ff = time.perf_counter()
     cam = rtp.default_camera()
     ids = torch.from_numpy(ids_np).cuda()
     out = torch.empty((npix, 4), dtype=torch.float32, device="cuda")
@@ -172,6 +243,10 @@ def main() -> None:
             render()
         return gather_canvas()
 
+    t_first = time.perf_counter()
+    render()
+    torch.cuda.synchronize()
+    t_first_done = time.perf_counter()
     for i in range(args.warmup):  # the first also counts live bounces (for the byte model)
         step(count_live=(i == 0))
     if args.warmup == 0:
@@ -206,6 +281,11 @@ def main() -> None:
         a, b = canvas[:, :3].cpu().numpy(), full[:, :3].cpu().numpy()
         same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
         check = bool(same.all())
+    quality = None
+    if rank == 0:
+        gold = load_golden_frame(args.golden)
+        if gold and (gold["nx"], gold["ny"], gold["spp"], gold["depth"]) == (nx, ny, args.spp, args.depth):
+            quality = frame_quality(canvas.cpu().numpy(), gold, args.spp)
     if world > 1:
         t = torch.tensor([elapsed, live_total], dtype=torch.float64,
                          device="cuda" if args.dist_backend == "nccl" else "cpu")
@@ -219,13 +299,24 @@ def main() -> None:
         live_all = float(live_total)
 
     samples_rank = npix * args.spp
-    samples_all = samples_rank * world
+    samples_all = nx * ny * args.spp
     value = samples_all * args.steps / elapsed / 1e6
     L = live_all / samples_all
     bytes_per_sample = 56.0 + 88.0 * L
     achieved = samples_rank * bytes_per_sample / (kernel_ms / 1e3) / 1e9
     cfg = {"nx": nx, "ny": args.ny, "spp": args.spp, "depth": args.depth}
-    traffic = load_traffic(args.traffic_json, cfg)
+    traffic = load_traffic(args.traffic_json, cfg) if world == 1 else None
+    valu = load_valu(args.valu_json, cfg, kernel_ms) if world == 1 else None
+    setup = {
+        "context_ms": round((t_ctx - t_setup) * 1e3, 2),
+        "scene_ms": round((t_scene - t_ctx) * 1e3, 2),
+        "ff_tables_ms": round((t_ff - t_scene) * 1e3, 2),
+        "ff_tables": {k: ff[k] for k in ("policy", "built", "chain_tables", "direct_first", "direct_count")}
+                     | {"gib": round(ff["bytes"] / 2**30, 1), "alloc_ms": round(ff["alloc_ms"], 1),
+                        "build_ms": round(ff["build_ms"], 1)},
+    }
+    first_ms = (t_first_done - t_first) * 1e3
+    e2e_s = t_first_done - t_setup
 
     if rank == 0:
         cpu = cpu_mt = None
@@ -233,6 +324,11 @@ def main() -> None:
             cpu = cpu_baseline(args.cpu_budget, args.nx, args.ny, args.depth)
         if world == 1 and args.cpu_budget_mt > 0:
             cpu_mt = cpu_baseline(args.cpu_budget_mt, args.nx, args.ny, args.depth, nthreads=host_threads())
+        if world == 1:
+            shard_desc = "one GPU: the whole frame"
+        else:
+            shard_desc = (f"{TILE}x{TILE} tiles round-robin over {world} ranks, 1 "
+                          + ("RCCL" if args.dist_backend == "nccl" else "gloo") + " reduce/step")
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -242,17 +338,28 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / max(args.steps, 1) * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32 (f64 mixture/pdf islands)",
             "data": "synthetic: the reference's deterministic Cornell Box scene and camera (main.cc:616-622), "
                     "seed = pixel index",
             "config": {
-                "workload": "C2: Cornell Box 800x800 per GPU, 1000 spp, depth 50",
+                "workload": "C2: Cornell Box 800x800, 1000 spp, depth 50" + ("" if strong or world == 1 else
+                                                                          f" per GPU (canvas {nx}x{ny})"),
                 "nx": nx, "ny": ny, "spp": args.spp, "depth": args.depth,
-                "pixels_per_gpu": npix, "shard": f"{TILE}x{TILE} tiles round-robin (" + ("pixel of each tile entry computed in-kernel" if tiled else "pixel list") + "), 1 RCCL reduce/step",
+                "pixels_per_gpu": npix,
+                "shard": shard_desc + (" (pixel of each tile entry computed in-kernel)" if tiled else " (pixel list)"),
                 "live_bounces_per_sample": round(L, 6),
             },
+            "rmse": None if quality is None else quality["rmse"],
+            "bit_exact": None if quality is None else quality["bit_exact"],
+            "quality": quality,
+            "setup": setup,
+            "first_render_ms": round(first_ms, 2),
+            "one_shot": {"end_to_end_ms": round(e2e_s * 1e3, 1),
+                         "msamples_per_s": round(samples_all / e2e_s / 1e6, 1),
+                         "note": "fresh context: create + scene + jump-table policy + first render (main.cc's "
+                                 "timer, :584-585, 661-663, minus process start)"},
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 3),
@@ -263,6 +370,7 @@ def main() -> None:
                 "kernel_ms": round(kernel_ms, 3),
                 "bytes_per_sample_model": round(bytes_per_sample, 3),
             },
+            "roofline_valu": valu,
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_mt,
         }

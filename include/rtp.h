@@ -5,7 +5,7 @@
  * (reference MapperPathTracer.h:44-159, MapperPathTracer.cxx:94-406).  Plain
  * pointers and sizes only; no VTK-m, HIP or torch types in the signatures.
  * The reference exposes a C++ class, so the "binding" a maintainer adds is
- * the header-only C++ shim include/rtp/mapper.hpp (same class and method
+ * the header-only C++ shim include/rtp/rendering.hpp (same class and method
  * names) -- see INTEGRATION.md.
  *
  * Mapping to the reference:
@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define RTP_ABI_VERSION 2
+#define RTP_ABI_VERSION 3
 
 typedef enum {
   RTP_OK = 0,
@@ -142,6 +142,19 @@ rtp_status rtp_render_device(rtp_context* ctx, const rtp_camera* cam, int32_t nx
                              const int64_t* d_pixel_ids, float* d_rgba_out, const rtp_pixel_aux* aux,
                              void* hip_stream, rtp_stats* stats);
 
+/* rtp_render_device with a wave plan: the launch runs n_waves persistent
+ * waves and wave w owns the entries [d_wave_begin[w], d_wave_begin[w+1]) of
+ * the pixel set (each range <= 128 entries; d_wave_begin: device
+ * int32[n_waves+1], non-decreasing, ending at pixel_count).  Grouping pixels
+ * of similar cost into the same wave keeps its lanes busy to the end (a
+ * pixel's samples are one sequential chain).  Results are identical to
+ * rtp_render_device for any plan.  Scenes without the sphere BVH only. */
+rtp_status rtp_render_planned_device(rtp_context* ctx, const rtp_camera* cam, int32_t nx, int32_t ny, int32_t spp,
+                                     int32_t depth, uint32_t seed_base, int64_t pixel_begin, int64_t pixel_count,
+                                     const int64_t* d_pixel_ids, const int32_t* d_wave_begin, int32_t n_waves,
+                                     float* d_rgba_out, const rtp_pixel_aux* aux, void* hip_stream,
+                                     rtp_stats* stats);
+
 /* Host-memory variant of rtp_render_device for an arbitrary pixel list
  * (golden pixel subsets); aux pointers are host arrays. */
 rtp_status rtp_render_pixels(rtp_context* ctx, const rtp_camera* cam, int32_t nx, int32_t ny, int32_t spp,
@@ -220,11 +233,50 @@ rtp_status rtp_write_pnm_depth(const char* path, const float* depth, int32_t nx,
 /* Diagnostics: the device powf restatement (glibc_powf.hpp) elementwise. */
 rtp_status rtp_eval_powf(rtp_context* ctx, const float* x, float y, float* out, int64_t n);
 
+/* ------------------------------------------------------------------------
+ * RNG jump tables.  A path that ends before depthcount still draws the
+ * reference's random numbers for every remaining depth;
+ * the renderer skips them with tables of the dead-depth map over all 2^32
+ * RNG states (chain tables for 32/16/8/4 depths, direct tables for the
+ * counts depth-50 samples mostly have: 224 GiB of HBM by default, built once
+ * per device and process, shared by its contexts).  Results are identical
+ * with and without them; they only change speed and setup cost.
+ *   RTP_FF_TABLES_AUTO  (default) build them before the launch that takes the
+ *                       samples launched on the device past the break-even
+ *                       count (setup time / time saved per sample; see
+ *                       rtp_ff_info.auto_samples): a one-shot render such as
+ *                       main.cc's never pays the setup
+ *   RTP_FF_TABLES_OFF   hash every dead depth on this context
+ *   RTP_FF_TABLES_ON    build now (a long-lived renderer / service)
+ * Environment: RTP_FF_POLICY=auto|on|off sets the default of new contexts. */
+typedef enum {
+  RTP_FF_TABLES_AUTO = 0,
+  RTP_FF_TABLES_OFF = 1,
+  RTP_FF_TABLES_ON = 2,
+} rtp_ff_policy;
+
+typedef struct {
+  int32_t policy;         /* this context's rtp_ff_policy */
+  int32_t built;          /* 1 when the device's tables exist */
+  int32_t chain_tables;   /* tables for 32, 16, 8, 4, ... dead depths */
+  int32_t direct_first;   /* direct tables for counts [direct_first, +direct_count) */
+  int32_t direct_count;
+  uint64_t bytes;         /* device memory the tables hold */
+  double alloc_ms;        /* host time of their allocation (includes the driver's clearing) */
+  double build_ms;        /* device time of the build kernel */
+  uint64_t samples_seen;  /* samples launched on the device by this process */
+  uint64_t auto_samples;  /* the AUTO policy's break-even count */
+} rtp_ff_info;
+
+rtp_status rtp_set_ff_tables(rtp_context* ctx, int32_t policy);
+rtp_status rtp_get_ff_tables(rtp_context* ctx, rtp_ff_info* out);
+
 /* Diagnostics: evaluate a device primitive elementwise (tests only).
  * kind 0: glibc-exact sinf port, 1: cosf port, 2: 1/sqrtf(x) (RMagnitude),
  * 3: wang32 (bit pattern in/out), 4 / 5: the RNG jump tables (state after
  * 16 / 32 dead depths; RTP_ERR_DEVICE if they are not built), 6: the state
- * after one dead depth.  in/out: n 4-byte elements, host memory. */
+ * after one dead depth, 7: the first direct table (direct_first depths).
+ * in/out: n 4-byte elements, host memory. */
 rtp_status rtp_eval_primitive(rtp_context* ctx, int32_t kind, const void* in, void* out, int64_t n);
 
 /* Diagnostics: with RTP_DEBUG_STATS=1 in the environment the render kernel

@@ -58,6 +58,14 @@ class RtpDirectDesc(ctypes.Structure):
 
 
 RTP_AOV_COLOR, RTP_AOV_NORMALS, RTP_AOV_ALBEDO = 1, 2, 4
+RTP_FF_TABLES_AUTO, RTP_FF_TABLES_OFF, RTP_FF_TABLES_ON = 0, 1, 2
+
+
+class RtpFfInfo(ctypes.Structure):
+    _fields_ = [("policy", ctypes.c_int32), ("built", ctypes.c_int32), ("chain_tables", ctypes.c_int32),
+                ("direct_first", ctypes.c_int32), ("direct_count", ctypes.c_int32), ("bytes", ctypes.c_uint64),
+                ("alloc_ms", ctypes.c_double), ("build_ms", ctypes.c_double), ("samples_seen", ctypes.c_uint64),
+                ("auto_samples", ctypes.c_uint64)]
 
 
 EXPORTED_SYMBOLS = [
@@ -65,7 +73,8 @@ EXPORTED_SYMBOLS = [
     "rtp_render_device", "rtp_render_tiles_device", "rtp_render_pixels", "rtp_normalize", "rtp_write_pnm", "rtp_cornell_box",
     "rtp_eval_primitive", "rtp_debug_counters", "rtp_verify_fast_math", "rtp_debug_closest_hit",
     "rtp_render_direct", "rtp_render_direct_device", "rtp_sample_color_table", "rtp_quad_scalars",
-    "rtp_cornell_point_field", "rtp_write_pnm_depth", "rtp_eval_powf",
+    "rtp_cornell_point_field", "rtp_write_pnm_depth", "rtp_eval_powf", "rtp_set_ff_tables", "rtp_get_ff_tables",
+    "rtp_render_planned_device",
 ]
 
 
@@ -136,6 +145,12 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
                                           ctypes.POINTER(i32p), ctypes.POINTER(ctypes.c_int32)]
     L.rtp_write_pnm_depth.argtypes = [ctypes.c_char_p, f32p, ctypes.c_int32, ctypes.c_int32]
     L.rtp_eval_powf.argtypes = [vp, f32p, ctypes.c_float, f32p, ctypes.c_int64]
+    L.rtp_render_planned_device.argtypes = [vp, ctypes.POINTER(RtpCamera), ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_int64,
+                                            ctypes.c_int64, vp, vp, ctypes.c_int32, vp, ctypes.POINTER(RtpPixelAux),
+                                            vp, ctypes.POINTER(RtpStats)]
+    L.rtp_set_ff_tables.argtypes = [vp, ctypes.c_int32]
+    L.rtp_get_ff_tables.argtypes = [vp, ctypes.POINTER(RtpFfInfo)]
     for name in EXPORTED_SYMBOLS:
         if name not in ("rtp_last_error", "rtp_abi_version", "rtp_destroy"):
             getattr(L, name).restype = ctypes.c_int32

@@ -24,6 +24,7 @@ struct rtp_context {
   rtp::DevSphereG* d_sph_geom = nullptr;
   rtp::DevSphere* d_sph_all = nullptr;
   bool use_bvh = false;
+  int ff_policy = 0;  // rtp_ff_policy (RNG jump tables)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // Completion of the last launch.  The history buffer and the progress
   // counter are per-context scratch, so a launch on any stream first waits

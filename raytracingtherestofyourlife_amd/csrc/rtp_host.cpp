@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -26,7 +27,8 @@ extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::K
                                         hipStream_t stream);
 extern "C" hipError_t rtp_launch_eval_primitive(int kind, const void* in, void* out, int64_t n, const uint32_t* tab,
                                                 uint32_t t1, uint32_t t2, hipStream_t stream);
-extern "C" hipError_t rtp_launch_build_ff_table(uint32_t* T, int steps, uint32_t t1, uint32_t t2, hipStream_t stream);
+extern "C" hipError_t rtp_launch_build_ff_tables(const rtp::FfBuildOut* out, int max_r, uint32_t t1, uint32_t t2,
+                                                 hipStream_t stream);
 extern "C" hipError_t rtp_build_bvh_gpu(const float4* d_cr, int n, float3 lo, float3 ext, rtp::BvhNode* d_nodes,
                                         rtp::DevSphereG* d_geom, hipStream_t stream);
 extern "C" hipError_t rtp_launch_eval_closest(const rtp::DevScene* scene, const float* rays, uint32_t* out,
@@ -112,11 +114,9 @@ void fill_quad(rtp::DevQuad& Q, v3 q, v3 r, v3 s, v3 t) {
   }
   // Kinds 1..6 are axis-plane rectangles: their masks force s = (r_I, t_J),
   // so e23 == -e01 and e21 == -e03 exactly and they are always exact
-  // parallelograms (the prefilter's exact test, quad_hit_axis, relies on
-  // it).  Should one ever fail the check, it is scanned as a general quad
-  // (kind 0: the full products, equal to the masked ones for finite inputs)
-  // and the prefilter stays on for the others.
-  if (Q.kind >= 1 && Q.kind <= 6 && !Q.para) Q.kind = 0;
+  // parallelograms (the prefilter's exact test, quad_hit_axis, relies on it;
+  // setup_prefilter re-checks Q.para).  An in-plane quad that is not a
+  // parallelogram has a non-rectangular mask set and is kind 0.
 }
 
 bool bit_equal(const float* a, const float* b, int n) { return std::memcmp(a, b, sizeof(float) * n) == 0; }
@@ -146,7 +146,7 @@ void setup_prefilter(rtp::DevScene* h, const rtp_scene_desc* s, const std::vecto
     const int flat = 7 & ~(K.m01 | K.m03);
     if (Q.kind < 1 || Q.kind > 6 || (flat != 1 && flat != 2 && flat != 4)) return;
     const int a = flat == 1 ? 0 : flat == 2 ? 1 : 2, b = (a + 1) % 3, c = (a + 2) % 3;
-    if (!Q.para) return;  // (unreachable: fill_quad moves non-parallelograms to kind 0)
+    if (!Q.para) return;  // (unreachable: kinds 1..6 are exact parallelograms, see fill_quad)
     {
       const int ei = K.m01 == 1 ? 0 : K.m01 == 2 ? 1 : 2, ej = K.m03 == 1 ? 0 : K.m03 == 2 ? 1 : 2;
       const int ea = 3 - ei - ej;
@@ -202,101 +202,135 @@ void setup_prefilter(rtp::DevScene* h, const rtp_scene_desc* s, const std::vecto
 // RNG jump tables.  A dead depth consumes 1 + {2,3,2} draws chosen by the
 // `which` draw against two constant thresholds (lightables = 2,
 // MapperPathTracer.cxx:218; PdfWorklet.h:20), so "advance the state over k
-// dead depths" is a fixed map of the 32-bit state.  Table j tabulates it for
-// k = 32 >> j over all 2^32 states (16 GiB each; built once per device and
-// process, shared by every context).  The pool kernel's fast-forward then
-// takes a few table reads instead of ~150 hashes per sample.  RTP_FF_TABLES=n
-// (0..6, default 4: 64 GiB) sets how many tables (32, 16, 8, 4, 2, 1 depths) to build;
-// fewer are built when the device lacks the memory (8 GiB kept free).  On C2,
-// 2 / 3 / 4 tables measured 170.8 / 168.9 / 169.8 ms per render before the
-// critical-pixel fast-forward trigger, and 3 / 4 tables 148.2 / 147.0 ms after
-// it; 4 / 5 / 6 tables (down to single dead steps, no hashing left) 146.7 /
-// 147.9 / 149.3 ms (3 interleaved rounds each, same box).
+// dead depths" is a fixed map of the 32-bit state.  Chain table j tabulates
+// it for k = 32 >> j over all 2^32 states (16 GiB each), and the direct
+// tables for each k in [d_first, d_first + d_count): a finished sample whose
+// remaining count falls in the direct block is fast-forwarded by ONE gather,
+// others by a chain of gathers plus a few hashed depths (rtp_render_pool).
+// Defaults: 4 chain tables (32, 16, 8, 4) and direct tables 41..50 (the
+// counts a depth-50 render's samples mostly have), 224 GiB in all;
+// RTP_FF_TABLES=n (0..6) / RTP_FF_DIRECT=n / RTP_FF_DIRECT_FIRST=r change
+// the set, and it shrinks to the free device memory (8 GiB kept free).
+// The tables are per device and process, shared by every context, and built
+// by the policy of rtp_set_ff_tables (include/rtp.h): what they cost
+// (allocation + build, measured here) against what they save per sample.
 struct FfTables {
   uint32_t* t[rtp::kFfTables] = {};
-  // direct tables: one per remaining-dead-depth count r in [d_first,
-  // d_first + d_count), contiguous (16 GiB each): a finished sample whose r
-  // falls in the range is fast-forwarded by ONE gather instead of a chain
-  uint32_t* direct = nullptr;
-  int d_first = 0, d_count = 0;
-  bool tried = false;
-  float build_ms = 0.f;
+  uint32_t* direct = nullptr;  // d_count tables of 2^32 entries, contiguous
+  int d_first = 0, d_count = 0, n_chain = 0;
+  bool built = false;
+  double alloc_ms = 0, build_ms = 0;
+  uint64_t bytes = 0;
+  uint64_t samples_seen = 0;  // samples launched on this device (the AUTO policy's count)
 };
 std::mutex g_ff_mu;
 FfTables g_ff[64];
 
-const FfTables& ff_tables(int device) {
-  std::lock_guard<std::mutex> lk(g_ff_mu);
-  FfTables& T = g_ff[device & 63];
-  if (T.tried) return T;
-  T.tried = true;
-  int want = 4;
+int ff_policy_default() {
+  const char* e = getenv("RTP_FF_POLICY");
+  if (e && !std::strcmp(e, "on")) return RTP_FF_TABLES_ON;
+  if (e && !std::strcmp(e, "off")) return RTP_FF_TABLES_OFF;
+  return RTP_FF_TABLES_AUTO;
+}
+
+// AUTO: build once the samples launched on the device (this launch included)
+// reach the break-even count: setup (allocation + build, ~0.6 s on MI355X;
+// DESIGN.md 4.1) over the kernel time the tables save per sample (C2: 147.6
+// vs 116.2 ms per 6.4e8 samples, 4.9e-11 s).  RTP_FF_AUTO_SAMPLES overrides.
+uint64_t ff_auto_samples() {
+  if (const char* e = getenv("RTP_FF_AUTO_SAMPLES")) return (uint64_t)std::strtoull(e, nullptr, 10);
+  return 12000000000ull;
+}
+
+void ff_free(FfTables& T) {
+  for (uint32_t*& p : T.t) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+  }
+  if (T.direct) (void)hipFree(T.direct);
+  T.direct = nullptr;
+  T.d_count = T.n_chain = 0;
+  T.bytes = 0;
+}
+
+// Allocate and build the tables of `device` now (caller holds g_ff_mu).
+void ff_build(FfTables& T) {
+  if (T.built) return;
+  T.built = true;
+  int want = 4, nd = 10, first = 41;
   if (const char* env = getenv("RTP_FF_TABLES")) want = std::max(0, std::min(rtp::kFfTables, atoi(env)));
-  const size_t bytes = (size_t)4 << 32;
+  if (const char* env = getenv("RTP_FF_DIRECT")) nd = std::max(0, std::min(32, atoi(env)));
+  if (const char* env = getenv("RTP_FF_DIRECT_FIRST")) first = std::max(1, atoi(env));
+  if (first + nd > rtp::kFfMaxSteps) nd = std::max(0, rtp::kFfMaxSteps - first);
+  const size_t bytes = (size_t)4 << 32, reserve = 8ull << 30;
+  auto fits = [&](size_t n) {
+    size_t free_b = 0, total_b = 0;
+    return hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b >= n + reserve;
+  };
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int j = 0; j < want; j++) {
+    if (!fits(bytes) || hipMalloc(&T.t[j], bytes) != hipSuccess) {
+      T.t[j] = nullptr;
+      break;
+    }
+    T.n_chain = j + 1;
+  }
+  if (want == 0) nd = 0;  // (RTP_FF_TABLES=0: no tables at all)
+  {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+      nd = std::min<int>(nd, free_b > reserve ? (int)((free_b - reserve) / bytes) : 0);
+    else
+      nd = 0;
+  }
+  if (nd > 0 && hipMalloc(&T.direct, bytes * (size_t)nd) == hipSuccess) {
+    T.d_first = first;
+    T.d_count = nd;
+  } else {
+    T.direct = nullptr;
+  }
+  (void)hipGetLastError();
+  T.alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  rtp::FfBuildOut out{};
+  int max_r = 0;
+  for (int j = 0; j < T.n_chain; j++) {
+    out.t[32 >> j] = T.t[j];
+    max_r = std::max(max_r, 32 >> j);
+  }
+  for (int k = 0; k < T.d_count; k++) {
+    out.t[first + k] = T.direct + (size_t)k * (bytes / 4);
+    max_r = std::max(max_r, first + k);
+  }
+  if (max_r == 0) return;
   const uint32_t t1 = which_threshold(2), t2 = which_threshold(3);
   hipEvent_t a = nullptr, b = nullptr;
-  if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return T;
-  (void)hipEventRecord(a, nullptr);
-  for (int j = 0; j < want; j++) {
-    size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < bytes + (8ull << 30)) break;
-    if (hipMalloc(&T.t[j], bytes) != hipSuccess) {
-      T.t[j] = nullptr;
-      break;
-    }
-    if (rtp_launch_build_ff_table(T.t[j], 32 >> j, t1, t2, nullptr) != hipSuccess) {
-      (void)hipFree(T.t[j]);
-      T.t[j] = nullptr;
-      break;
-    }
-  }
-  // Direct tables for the counts finished samples most often have.  With
-  // depth 50 a path ending at depth k leaves 49 - k dead depths (50 - k after
-  // a light hit), and paths end early (C2: 3.7 live bounces per sample), so
-  // the default block covers 41..50.  RTP_FF_DIRECT=n (0 disables) and
-  // RTP_FF_DIRECT_FIRST=r choose the block; it shrinks to the free memory.
-  if (T.t[0] != nullptr) {
-    int nd = 10, first = 41;
-    if (const char* env = getenv("RTP_FF_DIRECT")) nd = std::max(0, std::min(32, atoi(env)));
-    if (const char* env = getenv("RTP_FF_DIRECT_FIRST")) first = std::max(1, atoi(env));
-    size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
-      const size_t reserve = 8ull << 30;
-      const int fit = free_b > reserve ? (int)((free_b - reserve) / bytes) : 0;
-      nd = std::min(nd, fit);
-    } else {
-      nd = 0;
-    }
-    if (nd > 0 && hipMalloc(&T.direct, bytes * (size_t)nd) == hipSuccess) {
-      bool ok = true;
-      for (int k = 0; k < nd && ok; k++)
-        ok = rtp_launch_build_ff_table(T.direct + (size_t)k * (bytes / 4), first + k, t1, t2, nullptr) == hipSuccess;
-      if (ok) {
-        T.d_first = first;
-        T.d_count = nd;
-      } else {
-        (void)hipFree(T.direct);
-        T.direct = nullptr;
-      }
-    } else {
-      T.direct = nullptr;
-    }
-  }
-  (void)hipEventRecord(b, nullptr);
-  if (hipEventSynchronize(b) != hipSuccess) {
-    for (uint32_t*& p : T.t) {
-      if (p) (void)hipFree(p);
-      p = nullptr;
-    }
-    if (T.direct) (void)hipFree(T.direct);
-    T.direct = nullptr;
-    T.d_count = 0;
-  }
-  (void)hipEventElapsedTime(&T.build_ms, a, b);
-  (void)hipEventDestroy(a);
-  (void)hipEventDestroy(b);
+  bool ok = hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess;
+  ok = ok && hipEventRecord(a, nullptr) == hipSuccess;
+  ok = ok && rtp_launch_build_ff_tables(&out, max_r, t1, t2, nullptr) == hipSuccess;
+  ok = ok && hipEventRecord(b, nullptr) == hipSuccess && hipEventSynchronize(b) == hipSuccess;
+  float ms = 0;
+  if (ok) (void)hipEventElapsedTime(&ms, a, b);
+  if (a) (void)hipEventDestroy(a);
+  if (b) (void)hipEventDestroy(b);
   (void)hipGetLastError();
-  return T;
+  if (!ok) {
+    ff_free(T);
+    return;
+  }
+  T.build_ms = ms;
+  T.bytes = bytes * (size_t)(T.n_chain + T.d_count);
+}
+
+// The tables a launch of `samples` samples on `device` uses under `policy`
+// (built first when the policy says so).
+const FfTables& ff_tables(int device, int policy, uint64_t samples) {
+  std::lock_guard<std::mutex> lk(g_ff_mu);
+  FfTables& T = g_ff[device & 63];
+  T.samples_seen += samples;
+  if (!T.built && (policy == RTP_FF_TABLES_ON || (policy == RTP_FF_TABLES_AUTO && T.samples_seen >= ff_auto_samples())))
+    ff_build(T);
+  static const FfTables none{};
+  return policy == RTP_FF_TABLES_OFF ? none : T;
 }
 
 // Sphere BVH (replaces the VTK-m LinearBVH of buildBVH, MapperPathTracer.cxx:
@@ -466,6 +500,7 @@ rtp_status rtp_create(int32_t device, rtp_context** out) {
   HIP_TRY(hipSetDevice(device));
   rtp_context* c = new rtp_context();
   c->device = device;
+  c->ff_policy = ff_policy_default();
   e = hipMalloc(&c->d_scene, sizeof(rtp::DevScene));
   if (e != hipSuccess) {
     delete c;
@@ -809,7 +844,7 @@ rtp_status ensure_hist(rtp_context* c, size_t bytes) {
 rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny, int32_t spp, int32_t depth,
                   uint32_t seed_base, int64_t pixel_begin, int64_t npix, const int64_t* d_ids, float* d_out,
                   uint32_t* d_seed, uint32_t* d_live, hipStream_t stream, double* kernel_ms,
-                  const int32_t* tile = nullptr) {
+                  const int32_t* tile = nullptr, const int32_t* d_wave_begin = nullptr, int plan_waves = 0) {
   // the kernels index a launch's entries with 32-bit integers
   if (npix > INT32_MAX) return fail(RTP_ERR_INVALID_ARGUMENT, "render: more than 2^31-1 pixels in one launch");
   HIP_TRY(hipSetDevice(c->device));
@@ -825,15 +860,24 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
   p.seed_out = d_seed;
   p.live_out = d_live;
   int variant = 2, waves = 0;
-  const int64_t lanes = rtp_plan_history_lanes(npix, c->use_bvh ? 1 : 0, &variant, &waves);
-  size_t hist_need = (size_t)depth * (size_t)lanes * 16;  // D rows (row k of a light hit holds E_k)
+  int64_t lanes = rtp_plan_history_lanes(npix, c->use_bvh ? 1 : 0, &variant, &waves);
+  if (d_wave_begin) {  // a planned launch: the caller's waves
+    if (variant != 2 || c->use_bvh || tile)
+      return fail(RTP_ERR_INVALID_ARGUMENT, "render: a wave plan needs the pool kernel, no BVH, no tile deal");
+    waves = plan_waves;
+    lanes = (int64_t)plan_waves * 128;
+  }
+  p.wave_begin = d_wave_begin;
+  // D rows per lane (row k of a light hit holds E_k), rounded up to 8 (a
+  // slot-major history pads each slot to whole 128-byte lines)
+  size_t hist_need = (size_t)((depth + 7) & ~7) * (size_t)lanes * 16;
   rtp_status rs = ensure_hist(c, hist_need);
   if (rs != RTP_OK) return rs;
   p.hist = c->d_hist;
   p.dbg = nullptr;
   p.progress = c->d_progress;
   if (variant == 2) {
-    const FfTables& ft = ff_tables(c->device);
+    const FfTables& ft = ff_tables(c->device, c->ff_policy, (uint64_t)npix * (uint64_t)spp);
     for (int j = 0; j < rtp::kFfTables; j++) p.ff[j] = ft.t[j];
     p.ffd = ft.direct, p.ffd_first = ft.d_first, p.ffd_count = ft.d_count;
   }
@@ -971,6 +1015,29 @@ rtp_status rtp_render_device(rtp_context* c, const rtp_camera* cam, int32_t nx, 
   return rs;
 }
 
+// rtp_render_device with a wave plan (include/rtp.h).
+rtp_status rtp_render_planned_device(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny, int32_t spp,
+                                     int32_t depth, uint32_t seed_base, int64_t pixel_begin, int64_t pixel_count,
+                                     const int64_t* d_pixel_ids, const int32_t* d_wave_begin, int32_t n_waves,
+                                     float* d_rgba_out, const rtp_pixel_aux* aux, void* hip_stream, rtp_stats* stats) {
+  rtp_status rs = check_render_args(c, cam, nx, ny, spp, depth);
+  if (rs != RTP_OK) return rs;
+  if (pixel_count <= 0 || !d_rgba_out || !d_wave_begin || n_waves <= 0 || n_waves > (1 << 24))
+    return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_render_planned_device: bad plan / output");
+  if (!d_pixel_ids && (pixel_begin < 0 || pixel_begin + pixel_count > (int64_t)nx * ny))
+    return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_render_planned_device: pixel range outside the canvas");
+  double ms = 0;
+  rs = launch(c, cam, nx, ny, spp, depth, seed_base, pixel_begin, pixel_count, d_pixel_ids, d_rgba_out,
+              aux ? aux->final_seed : nullptr, aux ? aux->live_bounces : nullptr, (hipStream_t)hip_stream,
+              stats ? &ms : nullptr, nullptr, d_wave_begin, n_waves);
+  if (rs == RTP_OK && stats) {
+    *stats = rtp_stats{};
+    stats->samples = (uint64_t)pixel_count * (uint64_t)spp;
+    stats->kernel_ms = ms;
+  }
+  return rs;
+}
+
 // rtp_render_device over the rank's tiles of a round-robin 16x16 tile deal
 // (shard.tile_pixels) without a pixel list: the kernel computes each entry's
 // pixel, which saves the per-sample gather of its id.
@@ -1026,17 +1093,17 @@ int32_t rtp_debug_counters(rtp_context* c, uint64_t* out, int32_t n_out) {
 }
 
 rtp_status rtp_eval_primitive(rtp_context* c, int32_t kind, const void* in, void* out, int64_t n) {
-  if (!c || !in || !out || n < 0 || kind < 0 || kind > 6)
+  if (!c || !in || !out || n < 0 || kind < 0 || kind > 7)
     return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_eval_primitive: bad arguments");
   if (n == 0) return RTP_OK;
   HIP_TRY(hipSetDevice(c->device));
   const uint32_t* tab = nullptr;
-  if (kind == 4 || kind == 5) {
-    const FfTables& ft = ff_tables(c->device);
-    tab = kind == 4 ? ft.t[1] : ft.t[0];  // 16 / 32 dead depths
-    if (!tab) return fail(RTP_ERR_DEVICE, "rtp_eval_primitive: RNG jump tables are not built (RTP_FF_TABLE=0 or memory)");
+  if (kind == 4 || kind == 5 || kind == 7) {
+    const FfTables& ft = ff_tables(c->device, c->ff_policy, 0);
+    tab = kind == 4 ? ft.t[1] : kind == 5 ? ft.t[0] : ft.direct;  // 16 / 32 dead depths, direct_first
+    if (!tab) return fail(RTP_ERR_DEVICE, "rtp_eval_primitive: RNG jump tables are not built (policy or memory)");
   }
-  const int dk = kind <= 3 ? kind : (kind <= 5 ? 4 : 5);  // device kinds: 4 gather, 5 one dead step
+  const int dk = kind <= 3 ? kind : (kind == 6 ? 5 : 4);  // device kinds: 4 gather, 5 one dead step
   void *din = nullptr, *dout = nullptr;
   HIP_TRY(hipMalloc(&din, (size_t)n * 4));
   hipError_t e = hipMalloc(&dout, (size_t)n * 4);
@@ -1097,6 +1164,35 @@ rtp_status rtp_verify_fast_math(rtp_context* c, int32_t kind, uint32_t lo_bits, 
   (void)hipFree(d_first);
   *mismatches = bad;
   if (first_bad) *first_bad = first;
+  return RTP_OK;
+}
+
+rtp_status rtp_set_ff_tables(rtp_context* c, int32_t policy) {
+  if (!c || policy < RTP_FF_TABLES_AUTO || policy > RTP_FF_TABLES_ON)
+    return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_set_ff_tables: bad arguments");
+  c->ff_policy = policy;
+  if (policy == RTP_FF_TABLES_ON) {
+    HIP_TRY(hipSetDevice(c->device));
+    (void)ff_tables(c->device, policy, 0);  // build now, outside any timed render
+  }
+  return RTP_OK;
+}
+
+rtp_status rtp_get_ff_tables(rtp_context* c, rtp_ff_info* out) {
+  if (!c || !out) return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_get_ff_tables: bad arguments");
+  std::lock_guard<std::mutex> lk(g_ff_mu);
+  const FfTables& T = g_ff[c->device & 63];
+  *out = rtp_ff_info{};
+  out->policy = c->ff_policy;
+  out->built = (T.n_chain + T.d_count) > 0 ? 1 : 0;
+  out->chain_tables = T.n_chain;
+  out->direct_first = T.d_first;
+  out->direct_count = T.d_count;
+  out->bytes = T.bytes;
+  out->alloc_ms = T.alloc_ms;
+  out->build_ms = T.build_ms;
+  out->samples_seen = T.samples_seen;
+  out->auto_samples = ff_auto_samples();
   return RTP_OK;
 }
 

@@ -39,6 +39,9 @@
 #ifndef RTP_FF_MARGIN
 #define RTP_FF_MARGIN 12  // pool kernel: fast-forward when READY holds fewer than idle lanes + this
 #endif
+#ifndef RTP_HIST_SLOT
+#define RTP_HIST_SLOT 0
+#endif
 #ifndef RTP_CRIT_FF
 #define RTP_CRIT_FF 100  // pool kernel: lag (per mille of the wave's average samples) that makes a pixel critical
 #endif
@@ -776,7 +779,10 @@ RTP_DEV CKP& kparams() {
   return *pp;
 }
 typedef const __attribute__((address_space(1))) uint32_t GU32;
-template <bool kStats, bool kBvh, bool kTiles = false>
+// kPlan: a planned launch (KParams::wave_begin): wave w owns the entries
+// [wave_begin[w], wave_begin[w+1]) -- up to kPool of them, grouped by their
+// expected cost -- instead of the interleaved entries j * n_waves + w.
+template <bool kStats, bool kBvh, bool kTiles = false, bool kPlan = false>
 #if RTP_POOL_MAX_VGPR > 0
 #define RTP_POOL_VGPR_ATTR __attribute__((amdgpu_num_vgpr(RTP_POOL_MAX_VGPR)))
 #else
@@ -806,10 +812,17 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
   const uint32_t t1 = sc->which_t1, t2 = sc->which_t2;
   const int D = p.depth, S = p.spp;
   // slot j of wave w <-> list entry k = j * n_waves + w (pixels interleaved over waves)
-  const int64_t left = p.npix - w;
-  const int n_slots = left <= 0 ? 0 : (int)min<int64_t>(kPool, (left + n_waves - 1) / n_waves);
+  // or, planned, k = wave_begin[w] + j
+  int n_slots, wbase = 0;
+  if constexpr (kPlan) {
+    wbase = p.wave_begin[w];
+    n_slots = min(kPool, p.wave_begin[w + 1] - wbase);
+  } else {
+    const int64_t left = p.npix - w;
+    n_slots = left <= 0 ? 0 : (int)min<int64_t>(kPool, (left + n_waves - 1) / n_waves);
+  }
   for (int j = lane; j < n_slots; j += 64) {
-    const int64_t k = (int64_t)j * n_waves + w;
+    const int64_t k = kPlan ? (int64_t)(wbase + j) : (int64_t)j * n_waves + w;
     s_seed[j] = p.seed_base + (uint32_t)pixel_of<kTiles>(p, k);  // seeds[i] = i (MapperPathTracer.cxx:265-267)
     s_r[j] = 0.f;
     s_g[j] = 0.f;
@@ -825,12 +838,20 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
   int unfinished = n_slots;                // stats only: pixels with samples still to run
   unsigned long long t_tail = 0;
 
-  // attenuation history per pixel SLOT, [d][wave*kPool + slot], D rows: a
-  // pixel has one sample in flight, so its history survives until the
-  // fast-forward batch that computes the sample's radiance (row k of a
-  // light hit holds E_k)
+  // attenuation history per pixel SLOT, D rows: a pixel has one sample in
+  // flight, so its history survives until the fast-forward batch that
+  // computes the sample's radiance (row k of a light hit holds E_k)
+#if RTP_HIST_SLOT
+  // slot-major [wave*kPool + slot][row], kHistRows rows per slot: a path's
+  // rows 0..7 share one 128-byte line
+  const int D8 = (D + 7) & ~7;
+  float4* __restrict__ const hist_base = reinterpret_cast<float4*>(p.hist) + (int64_t)w * kPool * D8;
+  const int64_t stride = 1, slot_stride = D8;
+#else
+  // depth-major [d][wave*kPool + slot]
   float4* __restrict__ const hist_base = reinterpret_cast<float4*>(p.hist) + (int64_t)w * kPool;
-  const int64_t stride = (int64_t)n_waves * kPool;
+  const int64_t stride = (int64_t)n_waves * kPool, slot_stride = 1;
+#endif
   float4* __restrict__ hist = hist_base;  // per lane: hist_base + slot of its path
   const f3 eye = ld3(p.cam.eye);
 
@@ -897,7 +918,7 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
         f3 c;
         if (flags & kEndLight) {
           const int k_end = D - frem;  // a light hit ends the path: rem = D - 1 - k_end + 1
-          const float4* __restrict__ hp = hist_base + fslot;
+          const float4* __restrict__ hp = hist_base + fslot * slot_stride;
           const float4 e = hp[(int64_t)k_end * stride];
           float sx = e.x + 0.0f, sy = e.y + 0.0f, sz = e.z + 0.0f;
           // two history rows per trip, both loads in flight together; the
@@ -989,14 +1010,14 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
       if (r < take) {
         slot = q_ready[(ready_head + r) & (kPool - 1)];
         seed = s_seed[slot];
-        hist = hist_base + slot;
+        hist = hist_base + slot * slot_stride;
         // the camera and tile constants re-read from the kernel arguments
         // here (kparams): kept live through the loop they were SGPRs spilled
         // to VGPR lanes, ~30 v_readlane per refill (through the kernarg
         // segment pointer: &p would copy p to scratch)
         CKP& P = kparams();
         int pi, pj;
-        pixel_xy<kTiles>(P, slot * n_waves + w, pi, pj);  // (32-bit index: a 64-bit one spilled)
+        pixel_xy<kTiles>(P, kPlan ? wbase + slot : slot * n_waves + w, pi, pj);  // (32-bit index: a 64-bit one spilled)
         ps.dir = camera_ray(P.cam, pi, pj, P.nx, P.ny, seed);
         ps.org = ld3(P.cam.eye);
         ps.d = 0;
@@ -1084,7 +1105,7 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
   }
   wave_sync();
   for (int j = lane; j < n_slots; j += 64) {
-    const int64_t k = (int64_t)j * n_waves + w;
+    const int64_t k = kPlan ? (int64_t)(wbase + j) : (int64_t)j * n_waves + w;
     reinterpret_cast<float4*>(p.out)[k] = make_float4(s_r[j], s_g[j], s_b[j], 0.f);
     if (p.seed_out) p.seed_out[k] = s_seed[j];
     if (p.live_out) p.live_out[k] = s_live[j];
@@ -1134,14 +1155,23 @@ __global__ void __launch_bounds__(256) rtp_eval_closest_kernel(const DevScene* _
   w[6] = full;
 }
 
-// Dead-step jump table: T[s] = dead_step^steps(s) for s in [base, base+count).
-__global__ void rtp_build_ff_table_kernel(uint32_t* __restrict__ T, int steps, uint32_t t1, uint32_t t2, uint64_t base,
-                                          uint64_t count) {
+// RNG jump tables, all in one pass: thread s iterates the dead-step map from
+// state s (= base + i) up to max_r steps and, after step r, stores the state
+// into every table that tabulates r dead depths (out.t[r] != null: the chain
+// tables for 32 / 16 / 8 / 4 ... depths and the direct tables of the counts
+// a finished sample most often has).  The stores of a wave go to consecutive
+// states, so each is one coalesced 256-byte write; the build costs max_r dead
+// steps per state instead of the sum of every table's depth count.
+__global__ void __launch_bounds__(256) rtp_build_ff_tables_kernel(FfBuildOut out, int max_r, uint32_t t1, uint32_t t2,
+                                                                   uint64_t base, uint64_t count) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
   uint32_t s = (uint32_t)(base + i);
-  for (int k = 0; k < steps; k++) s = dead_step(s, t1, t2);
-  T[base + i] = s;
+  for (int r = 1; r <= max_r; r++) {
+    s = dead_step(s, t1, t2);
+    uint32_t* __restrict__ T = out.t[r];  // wave-uniform
+    if (T != nullptr) T[base + i] = s;
+  }
 }
 
 // Exhaustive equivalence check of a fast sequence against the IEEE operation
@@ -1228,7 +1258,11 @@ extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int bvh, int* variant_ou
     if (waves_out) *waves_out = (int)((npix + 63) / 64);
     return npix;
   }
-  const int64_t by_lanes = (npix + 63) / 64;
+  // pixels per wave when the launch cannot fill every resident wave with 64
+  // (experiments: RTP_WAVE_PIXELS)
+  int wave_px = 64;
+  if (const char* e = getenv("RTP_WAVE_PIXELS")) wave_px = std::max(1, std::min(64, atoi(e)));
+  const int64_t by_lanes = (npix + wave_px - 1) / wave_px;
   const int64_t by_pool = (npix + rtp::kPool - 1) / rtp::kPool;
   const char* st = getenv("RTP_DEBUG_STATS");
   int64_t W = std::min<int64_t>(by_lanes, pool_resident_waves(st && st[0] == '1', bvh != 0));
@@ -1261,7 +1295,11 @@ extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::K
     const char* st = getenv("RTP_DEBUG_STATS");
     const bool stats = p->dbg && st && st[0] == '1';
     const dim3 g((unsigned)blocks), b(256);
-    if (p->tile_world > 0) {  // the tile deal: its own instances, no stats variant
+    if (p->wave_begin) {  // a planned launch (pixel list or range, no BVH)
+      if (bvh || p->tile_world > 0) return hipErrorNotSupported;
+      if (stats) hipLaunchKernelGGL((rtp::rtp_render_pool<true, false, false, true>), g, b, 0, stream, scene, *p, waves);
+      else hipLaunchKernelGGL((rtp::rtp_render_pool<false, false, false, true>), g, b, 0, stream, scene, *p, waves);
+    } else if (p->tile_world > 0) {  // the tile deal: its own instances, no stats variant
       if (bvh) hipLaunchKernelGGL((rtp::rtp_render_pool<false, true, true>), g, b, 0, stream, scene, *p, waves);
       else hipLaunchKernelGGL((rtp::rtp_render_pool<false, false, true>), g, b, 0, stream, scene, *p, waves);
     } else if (stats && bvh) hipLaunchKernelGGL((rtp::rtp_render_pool<true, true>), g, b, 0, stream, scene, *p, waves);
@@ -1272,11 +1310,13 @@ extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::K
   return hipGetLastError();
 }
 
-extern "C" hipError_t rtp_launch_build_ff_table(uint32_t* T, int steps, uint32_t t1, uint32_t t2, hipStream_t stream) {
+extern "C" hipError_t rtp_launch_build_ff_tables(const rtp::FfBuildOut* out, int max_r, uint32_t t1, uint32_t t2,
+                                                 hipStream_t stream) {
+  if (max_r < 1 || max_r >= rtp::kFfMaxSteps) return hipErrorInvalidValue;
   const uint64_t total = 1ull << 32, chunk = 1ull << 30;
   for (uint64_t base = 0; base < total; base += chunk) {
-    hipLaunchKernelGGL(rtp::rtp_build_ff_table_kernel, dim3((unsigned)(chunk / 256)), dim3(256), 0, stream, T, steps,
-                       t1, t2, base, chunk);
+    hipLaunchKernelGGL(rtp::rtp_build_ff_tables_kernel, dim3((unsigned)(chunk / 256)), dim3(256), 0, stream, *out,
+                       max_r, t1, t2, base, chunk);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

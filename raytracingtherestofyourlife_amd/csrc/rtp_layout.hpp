@@ -190,6 +190,12 @@ struct DevCamera {
 };
 
 constexpr int kFfTables = 6;  // jump tables for 32, 16, 8, 4, 2, 1 dead depths (default 4 built)
+constexpr int kFfMaxSteps = 64;  // build kernel: tables for 1..63 dead depths
+// the fused table build's outputs: t[r] receives the state after r dead
+// depths (null: no table for r)
+struct FfBuildOut {
+  uint32_t* t[kFfMaxSteps];
+};
 
 struct KParams {
   DevCamera cam;
@@ -215,6 +221,8 @@ struct KParams {
   // r dead depths from s, for r in [ffd_first, ffd_first + ffd_count)
   const uint32_t* ffd;
   int32_t ffd_first, ffd_count;
+  // planned launch (nullable): wave w owns entries [wave_begin[w], wave_begin[w+1])
+  const int32_t* wave_begin;
 };
 
 // -direct mode (main.cc:120-251): one launch renders the requested AOVs of

@@ -24,7 +24,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _lib
-from ._lib import RtpCamera, RtpPixelAux, RtpSceneDesc, RtpStats, check
+from ._lib import RtpCamera, RtpFfInfo, RtpPixelAux, RtpSceneDesc, RtpStats, check
 
 
 class ErrorBadValue(ValueError):
@@ -311,6 +311,22 @@ class Device:
                                         ctypes.byref(st) if timed else None))
         return st
 
+    def render_planned_device(self, camera: Camera, nx: int, ny: int, spp: int, depth: int, out_ptr: int,
+                              pixel_count: int, wave_begin_ptr: int, n_waves: int, pixel_ids_ptr: int = 0,
+                              pixel_begin: int = 0, seed_base: int = 0, stream: int = 0, seed_ptr: int = 0,
+                              live_ptr: int = 0, timed: bool = False):
+        """rtp_render_planned_device: wave w owns entries [wave_begin[w], wave_begin[w+1])."""
+        aux = RtpPixelAux(ctypes.cast(seed_ptr, _lib.u32p) if seed_ptr else None,
+                          ctypes.cast(live_ptr, _lib.u32p) if live_ptr else None)
+        st = RtpStats()
+        cam = camera.to_c()
+        check(self._L.rtp_render_planned_device(self.handle, ctypes.byref(cam), nx, ny, spp, depth, seed_base,
+                                                pixel_begin, pixel_count, ctypes.c_void_p(pixel_ids_ptr or None),
+                                                ctypes.c_void_p(wave_begin_ptr), n_waves, ctypes.c_void_p(out_ptr),
+                                                ctypes.byref(aux), ctypes.c_void_p(stream or None),
+                                                ctypes.byref(st) if timed else None))
+        return st
+
     def render_tiles_device(self, camera: Camera, nx: int, ny: int, spp: int, depth: int, out_ptr: int,
                             rank: int, world: int, seed_base: int = 0, stream: int = 0, timed: bool = False):
         """Device-resident render of rank's tiles of the round-robin 16x16
@@ -321,6 +337,23 @@ class Device:
                                               world, ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream or None),
                                               ctypes.byref(st) if timed else None))
         return st
+
+    FF_POLICIES = {"auto": _lib.RTP_FF_TABLES_AUTO, "off": _lib.RTP_FF_TABLES_OFF, "on": _lib.RTP_FF_TABLES_ON}
+
+    def set_ff_tables(self, policy: str) -> dict:
+        """RNG jump-table policy of this context (include/rtp.h rtp_set_ff_tables):
+        'auto' (default), 'off', or 'on' (build now: a long-lived renderer).
+        Returns ff_info()."""
+        check(self._L.rtp_set_ff_tables(self.handle, self.FF_POLICIES[policy]))
+        return self.ff_info()
+
+    def ff_info(self) -> dict:
+        """The device's jump tables: policy, what is built, bytes, setup cost."""
+        i = RtpFfInfo()
+        check(self._L.rtp_get_ff_tables(self.handle, ctypes.byref(i)))
+        d = {k: getattr(i, k) for k, _ in RtpFfInfo._fields_}
+        d["policy"] = {v: k for k, v in self.FF_POLICIES.items()}.get(d["policy"], d["policy"])
+        return d
 
     DEBUG_COUNTERS = ("bounce_steps", "bounce_lanes", "ff_phases", "ff_lanes", "ff_iters", "cycles_bounce",
                       "cycles_ff", "cycles_total", "cycles_intersect", "cycles_bounce_call", "cycles_end",

@@ -36,7 +36,7 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version():
     import raytracingtherestofyourlife_amd as rtp
 
-    assert rtp.load().rtp_abi_version() == 2
+    assert rtp.load().rtp_abi_version() == 3
 
 
 def test_create_without_gpu_fails_cleanly():

@@ -117,12 +117,13 @@ def test_oracle_reproduces_c2_full_frame_rows(oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["contiguous", "tiles"])
-def test_hip_reproduces_c2_full_frame(device, path):
+@pytest.mark.parametrize("path,tables", [("contiguous", "off"), ("contiguous", "on"), ("tiles", "on")])
+def test_hip_reproduces_c2_full_frame(device, path, tables):
     """The whole C2 frame on the GPU -- the bench workload -- bit-exact against
     the oracle's frame (NaN-aware), final RNG states and live-bounce counts
     equal (SHA-256 of all 640,000), and the metric's quality gate:
-    per-pixel RMSE of the normalised frame < 1e-4 (it is 0)."""
+    per-pixel RMSE of the normalised frame < 1e-4 (it is 0).  With the RNG
+    jump tables off (every dead depth hashed) and on (include/rtp.h)."""
     import torch
 
     import raytracingtherestofyourlife_amd as rtp
@@ -130,6 +131,20 @@ def test_hip_reproduces_c2_full_frame(device, path):
 
     g = load_full_frame(os.path.join(GOLD, "c2_full.npz"))
     device.set_cornell_box(0)
+    before = device.ff_info()["policy"]
+    device.set_ff_tables(tables)
+    try:
+        _c2_full_frame(device, path, g)
+    finally:
+        device.set_ff_tables(before)
+
+
+def _c2_full_frame(device, path, g):
+    import torch
+
+    import raytracingtherestofyourlife_amd as rtp
+    from raytracingtherestofyourlife_amd import shard
+
     cam = rtp.default_camera()
     n = 800 * 800
     out = torch.zeros((n, 4), dtype=torch.float32, device="cuda")

@@ -1,8 +1,9 @@
-"""RNG jump tables (ff16 / ff32, rtp_host.cpp): the state after 16 / 32 dead
-depths for every 32-bit state.  Checked on random states against an
-independent numpy restatement of the dead-depth draw sequence (which draw,
-then 2 or 3 generator draws, PdfWorklet.h:9-215), itself checked against the
-oracle's Wang hash."""
+"""RNG jump tables (rtp_host.cpp, one fused build kernel): the state after 32 /
+16 / ... dead depths (chain tables) and after each count of the direct block,
+for every 32-bit state.  Checked on random states against an independent
+numpy restatement of the dead-depth draw sequence (which draw, then 2 or 3
+generator draws, PdfWorklet.h:9-215), itself checked against the oracle's
+Wang hash.  Also the table policy of include/rtp.h (rtp_set_ff_tables)."""
 from __future__ import annotations
 
 import json
@@ -32,6 +33,15 @@ def dead_np(s, t1, t2):
 
 
 @pytest.fixture(scope="module")
+def tables(device):
+    """The tables built (policy 'on'); the device's policy restored after."""
+    before = device.ff_info()["policy"]
+    info = device.set_ff_tables("on")
+    yield info
+    device.set_ff_tables(before)
+
+
+@pytest.fixture(scope="module")
 def states():
     rng = np.random.default_rng(7)
     edge = np.array([0, 1, 2**31, 2**32 - 1, 0xDEADBEEF], dtype=np.uint32)
@@ -49,11 +59,56 @@ def test_one_dead_step(device, states):
     assert np.array_equal(got, dead_np(states, np.uint32(t1), np.uint32(t2)))
 
 
+def test_policy_auto_leaves_one_shot_renders_alone():
+    """A fresh context on the default policy renders a small frame without
+    building (or using) tables; the samples are counted toward break-even."""
+    import raytracingtherestofyourlife_amd as rtp
+
+    d = rtp.Device(0)
+    try:
+        i0 = d.ff_info()
+        assert i0["policy"] == "auto"
+        if i0["built"]:
+            pytest.skip("tables already built in this process")
+        d.set_cornell_box(0)
+        d.render(rtp.default_camera(), 32, 32, 4, 10)
+        i1 = d.ff_info()
+        assert i1["built"] == 0 and i1["samples_seen"] == i0["samples_seen"] + 32 * 32 * 4
+    finally:
+        d.close()
+
+
 @pytest.mark.parametrize("kind,steps", [(4, 16), (5, 32)])
-def test_jump_tables(device, states, kind, steps):
+def test_jump_tables(device, tables, states, kind, steps):
     t1, t2 = json.load(open(os.path.join(GOLD, "kat.json")))["which_thresholds"]
     want = states.copy()
     for _ in range(steps):
         want = dead_np(want, np.uint32(t1), np.uint32(t2))
     got = device.eval_primitive(kind, states)
     assert np.array_equal(got, want)
+
+
+def test_direct_table(device, tables, states):
+    t1, t2 = json.load(open(os.path.join(GOLD, "kat.json")))["which_thresholds"]
+    r = tables["direct_first"]
+    assert tables["direct_count"] > 0 and r > 0
+    want = states.copy()
+    for _ in range(r):
+        want = dead_np(want, np.uint32(t1), np.uint32(t2))
+    assert np.array_equal(device.eval_primitive(7, states), want)
+
+
+def test_policy_on_reports_setup(device, tables):
+    i = device.ff_info()
+    assert i["policy"] == "on" and i["built"] == 1
+    assert i["bytes"] == (i["chain_tables"] + i["direct_count"]) * (4 << 32)
+    assert i["chain_tables"] == 4 and i["build_ms"] > 0 and i["alloc_ms"] > 0
+    assert i["auto_samples"] > 0
+
+
+def test_bad_policy(device):
+    import raytracingtherestofyourlife_amd as rtp
+    from raytracingtherestofyourlife_amd._lib import check
+
+    with pytest.raises(rtp.RtpError):
+        check(rtp.load().rtp_set_ff_tables(device.handle, 7))

@@ -136,10 +136,10 @@ def test_gpu_prefilter_bvh_scene_equals_exact(device):
 
 
 def test_gpu_prefilter_with_trapezoid_in_axis_plane(device):
-    """A scene whose axis-plane quads include a non-parallelogram (a
-    trapezoid in the plane z = const, scanned as a general quad): the
-    prefilter stays on for the other axis-plane quads and every hit equals
-    the exact scan's."""
+    """A scene with a non-parallelogram in an axis plane (a trapezoid in the
+    plane z = const).  Its edge masks {1, 2, 3, 1} match no rectangle kind,
+    so it is a kind-0 (general) quad, scanned exactly; the prefilter stays
+    on for the axis-plane rectangles and every hit equals the exact scan's."""
     import raytracingtherestofyourlife_amd as rtp
 
     cb = rtp.CornellBox(0)

@@ -9,14 +9,21 @@ ap.add_argument("--spp", type=int, default=100)
 ap.add_argument("--depth", type=int, default=50)
 ap.add_argument("--n", type=int, default=800)
 ap.add_argument("--variant", type=int, default=0)
+ap.add_argument("--world", type=int, default=1, help="render rank --rank's share of the 16x16 tile deal")
+ap.add_argument("--rank", type=int, default=0)
+ap.add_argument("--ff-tables", default="on", choices=["on", "auto", "off"])
 a = ap.parse_args()
-dev = rtp.Device(0); dev.set_cornell_box(a.variant)
-out = torch.zeros((a.n * a.n, 4), dtype=torch.float32, device="cuda")
-live = torch.zeros(a.n * a.n, dtype=torch.int32, device="cuda")
-st = dev.render_device(rtp.default_camera(), a.n, a.n, a.spp, a.depth, out.data_ptr(),
+dev = rtp.Device(0); dev.set_cornell_box(a.variant); dev.set_ff_tables(a.ff_tables)
+from raytracingtherestofyourlife_amd import shard
+ids = torch.from_numpy(shard.tile_pixels(a.n, a.n, a.rank, a.world)).cuda() if a.world > 1 else None
+npx = a.n * a.n if ids is None else ids.numel()
+out = torch.zeros((npx, 4), dtype=torch.float32, device="cuda")
+live = torch.zeros(npx, dtype=torch.int32, device="cuda")
+st = dev.render_device(rtp.default_camera(), a.n, a.n, a.spp, a.depth, out.data_ptr(), pixel_count=npx,
+                       pixel_ids_ptr=0 if ids is None else ids.data_ptr(),
                        stream=torch.cuda.current_stream().cuda_stream, live_ptr=live.data_ptr(), timed=True)
 c = dev.debug_counters()
-samples = a.n * a.n * a.spp
+samples = npx * a.spp
 L = live.to(torch.int64).sum().item()
 c.update(kernel_ms=st.kernel_ms, samples=samples, live_bounces=L,
          lanes_per_bounce_step=c["bounce_lanes"] / max(1, c["bounce_steps"]),

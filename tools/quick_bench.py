@@ -15,6 +15,7 @@ ap.add_argument("--variant", type=int, default=0)
 ap.add_argument("--tiles", action="store_true", help="the tile-deal instance bench.py runs (rank 0 of 1), no live counters")
 ap.add_argument("--world", type=int, default=1, help="--tiles: the deal over this many ranks")
 ap.add_argument("--rank", type=int, default=0, help="--tiles: the rank whose share is rendered")
+ap.add_argument("--ff-tables", default="on", choices=["on", "auto", "off"], help="RNG jump-table policy")
 ap.add_argument("--list-tiles", action="store_true", help="the pixel-list path over the tile deal's order")
 ap.add_argument("--list-contig", action="store_true", help="the pixel-list path over the contiguous order")
 a = ap.parse_args()
@@ -26,6 +27,7 @@ if a.list_tiles:
     ids = torch.from_numpy(shard.tile_pixels(a.nx, a.ny, 0, 1)).cuda()
 dev = rtp.Device(0)
 dev.set_cornell_box(a.variant)
+dev.set_ff_tables(a.ff_tables)
 cam = rtp.default_camera()
 n = a.nx * a.ny
 out = torch.zeros((n, 4), dtype=torch.float32, device="cuda")

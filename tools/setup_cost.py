@@ -28,6 +28,7 @@ ap.add_argument("--depth", type=int, default=50)
 ap.add_argument("--renders", type=int, default=3)
 ap.add_argument("--rank", type=int, default=0)
 ap.add_argument("--world", type=int, default=1)
+ap.add_argument("--ff-tables", default="auto", choices=["on", "auto", "off"], help="RNG jump-table policy")
 a = ap.parse_args()
 t_import = time.perf_counter() - t_start
 
@@ -37,6 +38,9 @@ t_create = time.perf_counter() - t
 t = time.perf_counter()
 dev.set_cornell_box(0)
 t_scene = time.perf_counter() - t
+t = time.perf_counter()
+dev.set_ff_tables(a.ff_tables)
+t_ff = time.perf_counter() - t
 cam = rtp.default_camera()
 n = a.nx * a.ny
 out = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
@@ -50,15 +54,16 @@ for r in range(a.renders):
     torch.cuda.synchronize()
     walls.append((time.perf_counter() - t) * 1e3)
     kms.append(st.kernel_ms)
-info = rtp.ff_info(dev) if hasattr(rtp, "ff_info") else None
+info = dev.ff_info()
 samples = n // a.world * a.spp
 print(json.dumps(dict(
     env={k: v for k, v in os.environ.items() if k.startswith("RTP_")},
     workload=f"{a.nx}x{a.ny}x{a.spp} depth {a.depth}, tiles rank {a.rank}/{a.world}",
     import_s=round(t_import, 3), create_ms=round(t_create * 1e3, 2), scene_ms=round(t_scene * 1e3, 2),
+    ff_policy_ms=round(t_ff * 1e3, 2),
     render_wall_ms=[round(x, 2) for x in walls], kernel_ms=[round(x, 2) for x in kms],
     first_render_msamples_s=round(samples / walls[0] / 1e3, 1),
-    end_to_end_msamples_s=round(samples / (t_create + t_scene + walls[0] / 1e3) / 1e6, 1),
+    end_to_end_msamples_s=round(samples / (t_create + t_scene + t_ff + walls[0] / 1e3) / 1e6, 1),
     steady_msamples_s=round(samples / min(kms[1:] or kms) / 1e3, 1),
     ff=info)), flush=True)
 dev.close()
