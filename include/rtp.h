@@ -241,10 +241,12 @@ rtp_status rtp_eval_powf(rtp_context* ctx, const float* x, float y, float* out, 
  * counts depth-50 samples mostly have: 224 GiB of HBM by default, built once
  * per device and process, shared by its contexts).  Results are identical
  * with and without them; they only change speed and setup cost.
- *   RTP_FF_TABLES_AUTO  (default) build them before the launch that takes the
- *                       samples launched on the device past the break-even
- *                       count (setup time / time saved per sample; see
- *                       rtp_ff_info.auto_samples): a one-shot render such as
+ *   RTP_FF_TABLES_AUTO  (default) build them in two stages, each before the
+ *                       launch that takes the samples launched on the device
+ *                       past its break-even count (setup time / time saved
+ *                       per sample): the chain tables (64 GiB) at
+ *                       auto_samples, the direct tables at
+ *                       auto_samples_direct.  A one-shot render such as
  *                       main.cc's never pays the setup
  *   RTP_FF_TABLES_OFF   hash every dead depth on this context
  *   RTP_FF_TABLES_ON    build now (a long-lived renderer / service)
@@ -257,7 +259,7 @@ typedef enum {
 
 typedef struct {
   int32_t policy;         /* this context's rtp_ff_policy */
-  int32_t built;          /* 1 when the device's tables exist */
+  int32_t built;          /* 0 none, 1 the chain tables, 2 chain + direct tables */
   int32_t chain_tables;   /* tables for 32, 16, 8, 4, ... dead depths */
   int32_t direct_first;   /* direct tables for counts [direct_first, +direct_count) */
   int32_t direct_count;
@@ -265,7 +267,8 @@ typedef struct {
   double alloc_ms;        /* host time of their allocation (includes the driver's clearing) */
   double build_ms;        /* device time of the build kernel */
   uint64_t samples_seen;  /* samples launched on the device by this process */
-  uint64_t auto_samples;  /* the AUTO policy's break-even count */
+  uint64_t auto_samples;  /* the AUTO policy's break-even counts: chain tables, */
+  uint64_t auto_samples_direct; /* direct tables (RTP_FF_AUTO_SAMPLES=chain[,direct]) */
 } rtp_ff_info;
 
 rtp_status rtp_set_ff_tables(rtp_context* ctx, int32_t policy);

@@ -65,7 +65,7 @@ class RtpFfInfo(ctypes.Structure):
     _fields_ = [("policy", ctypes.c_int32), ("built", ctypes.c_int32), ("chain_tables", ctypes.c_int32),
                 ("direct_first", ctypes.c_int32), ("direct_count", ctypes.c_int32), ("bytes", ctypes.c_uint64),
                 ("alloc_ms", ctypes.c_double), ("build_ms", ctypes.c_double), ("samples_seen", ctypes.c_uint64),
-                ("auto_samples", ctypes.c_uint64)]
+                ("auto_samples", ctypes.c_uint64), ("auto_samples_direct", ctypes.c_uint64)]
 
 
 EXPORTED_SYMBOLS = [

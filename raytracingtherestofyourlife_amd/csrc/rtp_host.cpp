@@ -218,7 +218,7 @@ struct FfTables {
   uint32_t* t[rtp::kFfTables] = {};
   uint32_t* direct = nullptr;  // d_count tables of 2^32 entries, contiguous
   int d_first = 0, d_count = 0, n_chain = 0;
-  bool built = false;
+  int stage = 0;  // built so far: 1 chain tables, 2 + direct tables
   double alloc_ms = 0, build_ms = 0;
   uint64_t bytes = 0;
   uint64_t samples_seen = 0;  // samples launched on this device (the AUTO policy's count)
@@ -233,13 +233,23 @@ int ff_policy_default() {
   return RTP_FF_TABLES_AUTO;
 }
 
-// AUTO: build once the samples launched on the device (this launch included)
-// reach the break-even count: setup (allocation + build, ~0.6 s on MI355X;
-// DESIGN.md 4.1) over the kernel time the tables save per sample (C2: 147.6
-// vs 116.2 ms per 6.4e8 samples, 4.9e-11 s).  RTP_FF_AUTO_SAMPLES overrides.
-uint64_t ff_auto_samples() {
-  if (const char* e = getenv("RTP_FF_AUTO_SAMPLES")) return (uint64_t)std::strtoull(e, nullptr, 10);
-  return 12000000000ull;
+// AUTO builds in two stages, each once the samples launched on the device
+// (this launch included) reach its break-even count: setup time over the
+// kernel time it saves per sample (C2 on MI355X, profiles/r03b_*):
+//  - chain tables (64 GiB): ~0.25 s setup, 147 -> 125 ms per 6.4e8 samples
+//    (3.4e-11 s/sample): 7.4e9 samples, ~12 C2 renders;
+//  - direct tables (+160 GiB): 2.5-5 s of allocation (the driver clears the
+//    memory) + 0.2 s build, 125 -> 117 ms (1.3e-11 s/sample): ~3e11
+//    samples, ~450 C2 renders.
+// RTP_FF_AUTO_SAMPLES=chain[,direct] overrides.
+void ff_auto_samples(uint64_t& chain, uint64_t& direct) {
+  chain = 7500000000ull;
+  direct = 300000000000ull;
+  if (const char* e = getenv("RTP_FF_AUTO_SAMPLES")) {
+    char* end = nullptr;
+    chain = std::strtoull(e, &end, 10);
+    direct = (end && *end == ',') ? std::strtoull(end + 1, nullptr, 10) : chain;
+  }
 }
 
 void ff_free(FfTables& T) {
@@ -253,71 +263,73 @@ void ff_free(FfTables& T) {
   T.bytes = 0;
 }
 
-// Allocate and build the tables of `device` now (caller holds g_ff_mu).
-void ff_build(FfTables& T) {
-  if (T.built) return;
-  T.built = true;
+// Allocate and build the tables of a device up to `stage` (caller holds
+// g_ff_mu): 1 the chain tables, 2 also the direct block.
+void ff_build(FfTables& T, int stage) {
+  if (T.stage >= stage) return;
   int want = 4, nd = 10, first = 41;
   if (const char* env = getenv("RTP_FF_TABLES")) want = std::max(0, std::min(rtp::kFfTables, atoi(env)));
   if (const char* env = getenv("RTP_FF_DIRECT")) nd = std::max(0, std::min(32, atoi(env)));
   if (const char* env = getenv("RTP_FF_DIRECT_FIRST")) first = std::max(1, atoi(env));
   if (first + nd > rtp::kFfMaxSteps) nd = std::max(0, rtp::kFfMaxSteps - first);
+  if (want == 0) nd = 0;  // (RTP_FF_TABLES=0: no tables at all)
   const size_t bytes = (size_t)4 << 32, reserve = 8ull << 30;
   auto fits = [&](size_t n) {
     size_t free_b = 0, total_b = 0;
     return hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b >= n + reserve;
   };
+  rtp::FfBuildOut out{};
+  int max_r = 0;
   const auto t0 = std::chrono::steady_clock::now();
-  for (int j = 0; j < want; j++) {
-    if (!fits(bytes) || hipMalloc(&T.t[j], bytes) != hipSuccess) {
-      T.t[j] = nullptr;
-      break;
+  if (T.stage < 1) {
+    for (int j = 0; j < want; j++) {
+      if (!fits(bytes) || hipMalloc(&T.t[j], bytes) != hipSuccess) {
+        T.t[j] = nullptr;
+        break;
+      }
+      T.n_chain = j + 1;
+      out.t[32 >> j] = T.t[j];
+      max_r = std::max(max_r, 32 >> j);
     }
-    T.n_chain = j + 1;
   }
-  if (want == 0) nd = 0;  // (RTP_FF_TABLES=0: no tables at all)
-  {
+  if (stage >= 2 && nd > 0) {
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
       nd = std::min<int>(nd, free_b > reserve ? (int)((free_b - reserve) / bytes) : 0);
     else
       nd = 0;
-  }
-  if (nd > 0 && hipMalloc(&T.direct, bytes * (size_t)nd) == hipSuccess) {
-    T.d_first = first;
-    T.d_count = nd;
-  } else {
-    T.direct = nullptr;
+    if (nd > 0 && hipMalloc(&T.direct, bytes * (size_t)nd) == hipSuccess) {
+      T.d_first = first;
+      T.d_count = nd;
+      for (int k = 0; k < nd; k++) {
+        out.t[first + k] = T.direct + (size_t)k * (bytes / 4);
+        max_r = std::max(max_r, first + k);
+      }
+    } else {
+      T.direct = nullptr;
+    }
   }
   (void)hipGetLastError();
-  T.alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  rtp::FfBuildOut out{};
-  int max_r = 0;
-  for (int j = 0; j < T.n_chain; j++) {
-    out.t[32 >> j] = T.t[j];
-    max_r = std::max(max_r, 32 >> j);
+  T.alloc_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  T.stage = stage;
+  if (max_r > 0) {
+    const uint32_t t1 = which_threshold(2), t2 = which_threshold(3);
+    hipEvent_t a = nullptr, b = nullptr;
+    bool ok = hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess;
+    ok = ok && hipEventRecord(a, nullptr) == hipSuccess;
+    ok = ok && rtp_launch_build_ff_tables(&out, max_r, t1, t2, nullptr) == hipSuccess;
+    ok = ok && hipEventRecord(b, nullptr) == hipSuccess && hipEventSynchronize(b) == hipSuccess;
+    float ms = 0;
+    if (ok) (void)hipEventElapsedTime(&ms, a, b);
+    if (a) (void)hipEventDestroy(a);
+    if (b) (void)hipEventDestroy(b);
+    (void)hipGetLastError();
+    if (!ok) {
+      ff_free(T);
+      return;
+    }
+    T.build_ms += ms;
   }
-  for (int k = 0; k < T.d_count; k++) {
-    out.t[first + k] = T.direct + (size_t)k * (bytes / 4);
-    max_r = std::max(max_r, first + k);
-  }
-  if (max_r == 0) return;
-  const uint32_t t1 = which_threshold(2), t2 = which_threshold(3);
-  hipEvent_t a = nullptr, b = nullptr;
-  bool ok = hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess;
-  ok = ok && hipEventRecord(a, nullptr) == hipSuccess;
-  ok = ok && rtp_launch_build_ff_tables(&out, max_r, t1, t2, nullptr) == hipSuccess;
-  ok = ok && hipEventRecord(b, nullptr) == hipSuccess && hipEventSynchronize(b) == hipSuccess;
-  float ms = 0;
-  if (ok) (void)hipEventElapsedTime(&ms, a, b);
-  if (a) (void)hipEventDestroy(a);
-  if (b) (void)hipEventDestroy(b);
-  (void)hipGetLastError();
-  if (!ok) {
-    ff_free(T);
-    return;
-  }
-  T.build_ms = ms;
   T.bytes = bytes * (size_t)(T.n_chain + T.d_count);
 }
 
@@ -327,8 +339,14 @@ const FfTables& ff_tables(int device, int policy, uint64_t samples) {
   std::lock_guard<std::mutex> lk(g_ff_mu);
   FfTables& T = g_ff[device & 63];
   T.samples_seen += samples;
-  if (!T.built && (policy == RTP_FF_TABLES_ON || (policy == RTP_FF_TABLES_AUTO && T.samples_seen >= ff_auto_samples())))
-    ff_build(T);
+  if (policy == RTP_FF_TABLES_ON) {
+    ff_build(T, 2);
+  } else if (policy == RTP_FF_TABLES_AUTO) {
+    uint64_t chain = 0, direct = 0;
+    ff_auto_samples(chain, direct);
+    if (T.samples_seen >= direct) ff_build(T, 2);
+    else if (T.samples_seen >= chain) ff_build(T, 1);
+  }
   static const FfTables none{};
   return policy == RTP_FF_TABLES_OFF ? none : T;
 }
@@ -1184,7 +1202,7 @@ rtp_status rtp_get_ff_tables(rtp_context* c, rtp_ff_info* out) {
   const FfTables& T = g_ff[c->device & 63];
   *out = rtp_ff_info{};
   out->policy = c->ff_policy;
-  out->built = (T.n_chain + T.d_count) > 0 ? 1 : 0;
+  out->built = T.d_count > 0 ? 2 : T.n_chain > 0 ? 1 : 0;
   out->chain_tables = T.n_chain;
   out->direct_first = T.d_first;
   out->direct_count = T.d_count;
@@ -1192,7 +1210,10 @@ rtp_status rtp_get_ff_tables(rtp_context* c, rtp_ff_info* out) {
   out->alloc_ms = T.alloc_ms;
   out->build_ms = T.build_ms;
   out->samples_seen = T.samples_seen;
-  out->auto_samples = ff_auto_samples();
+  uint64_t chain = 0, direct = 0;
+  ff_auto_samples(chain, direct);
+  out->auto_samples = chain;
+  out->auto_samples_direct = direct;
   return RTP_OK;
 }
 

@@ -202,6 +202,12 @@ RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
 // absent, the compiler merged the LDS and global reads of the hit's record
 // into 7 flat loads (waited on both counters); now they are 2 ds_read_b128.
 constexpr int kLdsQuads = kMaxQuads, kQShadeFloats = 8;  // per quad: n, alb, mt, pad
+// The block's LDS table also holds the prefilter's PreExact records (after
+// the shading data): the candidate's record is then 4 ds_read_b128 instead of
+// 4 global loads (L2 hits) on every bounce's critical path (C2 kernel -1.7%,
+// r03c; an LDS copy of the quads in round 1 had been slower).
+constexpr int kPrexLdsOffset = kLdsQuads * kQShadeFloats;
+constexpr int kQTableFloats = kPrexLdsOffset + kMaxPre * 16;
 
 RTP_DEV void fill_qshade(const DevScene* __restrict__ sc, float* s_qshade) {
   for (int i = threadIdx.x; i < sc->n_quads * kQShadeFloats; i += blockDim.x) {
@@ -209,6 +215,8 @@ RTP_DEV void fill_qshade(const DevScene* __restrict__ sc, float* s_qshade) {
     const int f = i % kQShadeFloats;
     s_qshade[i] = f < 3 ? Q.n[f] : f < 6 ? Q.alb[f - 3] : f == 6 ? __int_as_float(Q.mt) : 0.f;
   }
+  const float* px = reinterpret_cast<const float*>(sc->prex);
+  for (int i = threadIdx.x; i < sc->n_pre * 16; i += blockDim.x) s_qshade[kPrexLdsOffset + i] = px[i];
 }
 
 // Closest-hit prefilter over the axis-plane quads (kinds 1..6).
@@ -336,7 +344,7 @@ RTP_DEV bool quad_hit_axis(const PreExact& E, f3 o, f3 d, float& t_out) {
 
 template <bool kBvh>
 RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefilter = false,
-                        uint32_t* full_out = nullptr) {
+                        uint32_t* full_out, const float* lds_prex) {
   Hit h{3.40282347e+38f, -1, 0};
   const float tmin = 0.001f;
   // the (t, orig) key minimum: the order the kinds are scanned in is free
@@ -366,13 +374,12 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
     pre_axis<0>(sc, p0, p1, o, d, ma, mb, k1, k2, pcur);
     pre_axis<1>(sc, p1, p2, o, d, ma, mb, k1, k2, pcur);
     pre_axis<2>(sc, p2, p3, o, d, ma, mb, k1, k2, pcur);
-    // the candidate's PreExact record: four 16-byte per-lane loads issued
-    // together (every lane: k1 = ~0u reads record 31, in bounds, unused);
-    // field-wise they compiled to ~4 dependent load / s_waitcnt vmcnt round
-    // trips.  (Issuing them before the exact scan above ran out of VGPRs.)
+    // the candidate's PreExact record from the block's LDS table: four
+    // 16-byte reads issued together (every lane: k1 = ~0u reads record 31,
+    // in bounds, unused)
     typedef float f4v __attribute__((ext_vector_type(4)));
-    const auto* gx = (const __attribute__((address_space(1))) f4v*)(sc->prex) + 4 * (k1 & 31u);
-    f4v xr[4] = {gx[0], gx[1], gx[2], gx[3]};
+    const f4v* lx = reinterpret_cast<const f4v*>(lds_prex) + 4 * (k1 & 31u);
+    f4v xr[4] = {lx[0], lx[1], lx[2], lx[3]};
     static_assert(sizeof(PreExact) == sizeof(xr), "PreExact is four 16-byte loads");
     if (lane_ok && k1 != ~0u) {  // (finite o, d: the generic arithmetic equals the kind's)
       PreExact Q;
@@ -464,7 +471,7 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
   const int d = ps.d;
   // intersect + CollectIntersecttWorklet (SurfaceWorklets.h:104-109)
   uint32_t fb = 0;  // (stats) 1: this lane ran the exact scan of the prefiltered quads
-  Hit h = closest_hit<kBvh>(sc, org, dir, true, st ? &fb : nullptr);
+  Hit h = closest_hit<kBvh>(sc, org, dir, true, st ? &fb : nullptr, qshade + kPrexLdsOffset);
   if (st) {
     const unsigned long long m = __ballot(fb == 1u);
     dbg[kDbgFallbackSteps] += m ? 1 : 0;
@@ -661,7 +668,7 @@ RTP_DEV int64_t pixel_of(const KP& p, int k) {  // k < npix <= INT32_MAX (launch
 // ------------------------------------------------------------------ v1 ---
 template <bool kBvh>
 __global__ void __launch_bounds__(256) rtp_render_lockstep(const DevScene* __restrict__ sc, KParams p) {
-  __shared__ __align__(16) float s_qshade[kLdsQuads * kQShadeFloats];
+  __shared__ __align__(16) float s_qshade[kQTableFloats];
   fill_qshade(sc, s_qshade);
   __syncthreads();
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -790,7 +797,7 @@ template <bool kStats, bool kBvh, bool kTiles = false, bool kPlan = false>
 #endif
 __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_ATTR rtp_render_pool(const DevScene* __restrict__ sc, KParams p, int n_waves) {
   __shared__ __align__(16) unsigned char smem[kPoolLdsBytes];
-  __shared__ __align__(16) float s_qshade[kLdsQuads * kQShadeFloats];
+  __shared__ __align__(16) float s_qshade[kQTableFloats];
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
   const int w = blockIdx.x * kWavesPerBlock + wib;  // global wave id
@@ -1139,7 +1146,7 @@ template <bool kBvh>
 __global__ void __launch_bounds__(256) rtp_eval_closest_kernel(const DevScene* __restrict__ sc,
                                                                const float* __restrict__ rays, uint32_t* out,
                                                                int64_t n) {
-  __shared__ __align__(16) float s_qshade[kLdsQuads * kQShadeFloats];
+  __shared__ __align__(16) float s_qshade[kQTableFloats];
   fill_qshade(sc, s_qshade);
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1147,8 +1154,8 @@ __global__ void __launch_bounds__(256) rtp_eval_closest_kernel(const DevScene* _
   const float* r = rays + 6 * i;
   const f3 o = mk(r[0], r[1], r[2]), d = mk(r[3], r[4], r[5]);
   uint32_t full = 0;
-  const Hit a = closest_hit<kBvh>(sc, o, d, true, &full);
-  const Hit b = closest_hit<kBvh>(sc, o, d);
+  const Hit a = closest_hit<kBvh>(sc, o, d, true, &full, s_qshade + kPrexLdsOffset);
+  const Hit b = closest_hit<kBvh>(sc, o, d, false, nullptr, nullptr);
   uint32_t* w = out + 7 * i;
   w[0] = __float_as_uint(a.t), w[1] = (uint32_t)a.kind, w[2] = (uint32_t)a.idx;
   w[3] = __float_as_uint(b.t), w[4] = (uint32_t)b.kind, w[5] = (uint32_t)b.idx;
