@@ -343,7 +343,7 @@ RTP_DEV bool quad_hit_axis(const PreExact& E, f3 o, f3 d, float& t_out) {
 }
 
 template <bool kBvh>
-RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefilter = false,
+RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefilter,
                         uint32_t* full_out, const float* lds_prex) {
   Hit h{3.40282347e+38f, -1, 0};
   const float tmin = 0.001f;
