@@ -23,6 +23,8 @@ struct rtp_context {
   rtp::BvhNode* d_nodes = nullptr;
   rtp::DevSphereG* d_sph_geom = nullptr;
   rtp::DevSphere* d_sph_all = nullptr;
+  rtp::LdsBvhNode* d_lnodes = nullptr;  // the LDS walk's copy of the tree (small BVH scenes)
+  int n_lnodes = 0;
   bool use_bvh = false;
   int ff_policy = 0;  // rtp_ff_policy (RNG jump tables)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;

@@ -24,7 +24,7 @@
 
 extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int bvh, int* variant_out, int* waves_out);
 extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::KParams* p, int variant, int waves, int bvh,
-                                        hipStream_t stream);
+                                        hipStream_t stream, int n_lnodes);
 extern "C" hipError_t rtp_launch_eval_primitive(int kind, const void* in, void* out, int64_t n, const uint32_t* tab,
                                                 uint32_t t1, uint32_t t2, hipStream_t stream);
 extern "C" hipError_t rtp_launch_build_ff_tables(const rtp::FfBuildOut* out, int max_r, uint32_t t1, uint32_t t2,
@@ -488,6 +488,57 @@ void bvh_flatten(const std::vector<TNode>& T, int t, int oct, const std::vector<
   out[me] = nd;
 }
 
+// The LDS walk's layout of the SAH tree (rtp_layout.hpp LdsBvhNode): nodes
+// numbered breadth-first with each inner node's children allocated as an
+// adjacent pair.  Only for trees whose leaves hold one sphere each and that
+// fit kLdsBvhMaxNodes; returns false otherwise.
+bool bvh_lds_layout(const std::vector<TNode>& T, const std::vector<int32_t>& order,
+                    const std::vector<rtp::DevSphere>& sph, std::vector<rtp::LdsBvhNode>& out) {
+  out.clear();
+  if (T.empty() || (int)T.size() > rtp::kLdsBvhMaxNodes) return false;
+  for (const TNode& t : T)
+    if (t.left < 0 && t.count != 1) return false;
+  out.resize(T.size());
+  std::vector<int> slot_of(T.size(), -1), queue{0};
+  slot_of[0] = 0;
+  int next = 1;
+  auto fill = [&](int t, int me, int parent, int paxis, int right) {
+    rtp::LdsBvhNode& nd = out[me];
+    std::memset(&nd, 0, sizeof(nd));
+    const TNode& s = T[t];
+    int32_t link = (parent & 0xffff) | (s.axis & 3) << 16 | (paxis & 3) << 18 | (right & 1) << 20;
+    if (s.left < 0) {
+      const rtp::DevSphere& S = sph[order[s.first]];
+      std::memcpy(nd.a, S.c, sizeof(nd.a));
+      nd.b[0] = S.rr;
+      const int32_t orig = order[s.first];
+      std::memcpy(&nd.b[1], &orig, sizeof(orig));
+      link |= 1 << 21;
+      nd.left = -1;
+    } else {
+      std::memcpy(nd.a, s.lo, sizeof(nd.a));
+      std::memcpy(nd.b, s.hi, sizeof(nd.b));
+    }
+    nd.link = link;
+  };
+  fill(0, 0, 0xffff, 0, 0);
+  for (size_t qi = 0; qi < queue.size(); qi++) {
+    const int t = queue[qi], me = slot_of[t];
+    const TNode& s = T[t];
+    if (s.left < 0) continue;
+    const int L = next;
+    next += 2;
+    out[me].left = L;
+    slot_of[s.left] = L;
+    slot_of[s.right] = L + 1;
+    fill(s.left, L, me, s.axis, 0);
+    fill(s.right, L + 1, me, s.axis, 1);
+    queue.push_back(s.left);
+    queue.push_back(s.right);
+  }
+  return next == (int)T.size();
+}
+
 }  // namespace
 
 // error reporting for the other translation units of librtp.so
@@ -548,6 +599,7 @@ void rtp_destroy(rtp_context* c) {
   if (c->d_nodes) (void)hipFree(c->d_nodes);
   if (c->d_sph_geom) (void)hipFree(c->d_sph_geom);
   if (c->d_sph_all) (void)hipFree(c->d_sph_all);
+  if (c->d_lnodes) (void)hipFree(c->d_lnodes);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->done) (void)hipEventDestroy(c->done);
@@ -680,6 +732,7 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
   }
   std::vector<rtp::BvhNode> nodes;
   std::vector<rtp::DevSphereG> geom;
+  std::vector<rtp::LdsBvhNode> lnodes;
   if (!use_bvh) {
     for (int k = 0; k < s->n_spheres; k++) h->spheres[k] = sph[k];
   } else if (gpu_build) {
@@ -699,6 +752,8 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     std::vector<int32_t> order;
     std::vector<TNode> tree;
     bvh_build(P, 0, s->n_spheres, tree, order);
+    const char* le = getenv("RTP_BVH_LDS");
+    if (!(le && le[0] == '0') && bvh_lds_layout(tree, order, sph, lnodes)) h->n_lnodes = (int32_t)lnodes.size();
     for (int oct = 0; oct < 8; oct++) {  // 8 copies of n_nodes entries, indices local to each copy
       std::vector<rtp::BvhNode> one;
       bvh_flatten(tree, 0, oct, order, sph, one);
@@ -752,7 +807,7 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     if (e == hipSuccess) e = hipEventSynchronize(c->done);
     c->pending = false;
   }
-  for (void** p : {(void**)&c->d_nodes, (void**)&c->d_sph_geom, (void**)&c->d_sph_all})
+  for (void** p : {(void**)&c->d_nodes, (void**)&c->d_sph_geom, (void**)&c->d_sph_all, (void**)&c->d_lnodes})
     if (*p && e == hipSuccess) {
       e = hipFree(*p);
       *p = nullptr;
@@ -791,11 +846,18 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
       e = hipMemcpy(c->d_sph_geom, geom.data(), geom.size() * sizeof(rtp::DevSphereG), hipMemcpyHostToDevice);
     if (e == hipSuccess)
       e = hipMemcpy(c->d_sph_all, sph.data(), sph.size() * sizeof(rtp::DevSphere), hipMemcpyHostToDevice);
+    if (e == hipSuccess && !lnodes.empty()) {
+      e = hipMalloc(&c->d_lnodes, lnodes.size() * sizeof(rtp::LdsBvhNode));
+      if (e == hipSuccess)
+        e = hipMemcpy(c->d_lnodes, lnodes.data(), lnodes.size() * sizeof(rtp::LdsBvhNode), hipMemcpyHostToDevice);
+    }
     h->nodes = c->d_nodes;
     h->sph_geom = c->d_sph_geom;
     h->sph_all = c->d_sph_all;
+    h->lnodes = c->d_lnodes;
   }
   if (e == hipSuccess) e = hipMemcpy(c->d_scene, h, sizeof(*h), hipMemcpyHostToDevice);
+  c->n_lnodes = h->n_lnodes;
   delete h;
   c->use_bvh = use_bvh;
   if (e != hipSuccess) return hip_fail(e, "rtp_set_scene upload");
@@ -878,7 +940,12 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
   p.seed_out = d_seed;
   p.live_out = d_live;
   int variant = 2, waves = 0;
-  int64_t lanes = rtp_plan_history_lanes(npix, c->use_bvh ? 1 : 0, &variant, &waves);
+  // the sphere BVH's walk: 2 out of LDS when the tree fits (rtp_render_pool_lds),
+  // 1 the global threaded walk (also for the diagnostics build and wave plans)
+  const char* stats_env = getenv("RTP_DEBUG_STATS");
+  const bool stats_on = stats_env && stats_env[0] == '1';
+  const int bvh = !c->use_bvh ? 0 : (c->n_lnodes > 0 && !stats_on && !d_wave_begin) ? 2 : 1;
+  int64_t lanes = rtp_plan_history_lanes(npix, bvh, &variant, &waves);
   if (d_wave_begin) {  // a planned launch: the caller's waves
     if (variant != 2 || c->use_bvh || tile)
       return fail(RTP_ERR_INVALID_ARGUMENT, "render: a wave plan needs the pool kernel, no BVH, no tile deal");
@@ -913,7 +980,7 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
     }
   }
   if (kernel_ms) HIP_TRY(hipEventRecord(c->ev0, stream));
-  HIP_TRY(rtp_launch_render(c->d_scene, &p, variant, waves, c->use_bvh ? 1 : 0, stream));
+  HIP_TRY(rtp_launch_render(c->d_scene, &p, variant, waves, bvh, stream, c->n_lnodes));
   HIP_TRY(hipEventRecord(c->done, stream));
   c->pending = true;
   if (kernel_ms) {

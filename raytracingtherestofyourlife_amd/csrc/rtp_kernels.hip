@@ -196,6 +196,76 @@ RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
   }
 }
 
+// The same closest-sphere search over the block's LDS copy of the tree
+// (LdsBvhNode, one copy for every direction): a stackless walk with parent
+// links (Hapala, Sassa, Pfister 2011).  State fromParent: `cur` was entered
+// from its parent (it is the near child); fromSibling: it is the far child,
+// entered after the near one's subtree; fromChild: `cur`'s subtree is done.
+// A node is tested on entry -- the slab test against [0, best t] with the
+// slack of spheres_bvh, or, for a leaf, its sphere -- and the walk descends
+// into a hit inner node's near child (on the side the ray comes from along
+// its split axis).  Each step is one 32-byte LDS read.
+RTP_DEV void spheres_bvh_lds(const LdsBvhNode* __restrict__ nodes, f3 o, f3 d, Hit& h) {
+  const float tmin = 0.001f;
+  const float ix = __builtin_amdgcn_rcpf(fabsf(d.x) < 1e-20f ? copysignf(1e-20f, d.x) : d.x);
+  const float iy = __builtin_amdgcn_rcpf(fabsf(d.y) < 1e-20f ? copysignf(1e-20f, d.y) : d.y);
+  const float iz = __builtin_amdgcn_rcpf(fabsf(d.z) < 1e-20f ? copysignf(1e-20f, d.z) : d.z);
+  const uint32_t neg = (d.x < 0.f ? 1u : 0u) | (d.y < 0.f ? 2u : 0u) | (d.z < 0.f ? 4u : 0u);
+  auto accept = [&](float t, int orig) {
+    if (t < h.t || (t == h.t && h.kind == 1 && orig < h.idx)) {
+      h.t = t;
+      h.kind = 1;
+      h.idx = orig;
+    }
+  };
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v* nv = reinterpret_cast<const f4v*>(nodes);
+  enum { kFromParent = 0, kFromSibling = 1, kFromChild = 2 };
+  int cur = 0, state = kFromParent;
+  for (;;) {
+    const f4v A = nv[2 * cur], B = nv[2 * cur + 1];
+    const int link = __float_as_int(A.w), left = __float_as_int(B.w);
+    const bool right = (link >> 20) & 1;
+    if (state == kFromChild) {
+      if (cur == 0) break;
+      // done with cur's subtree: its far sibling next if cur is the near child
+      const bool was_near = (uint32_t)right == ((neg >> ((link >> 18) & 3)) & 1u);
+      if (was_near) {
+        cur = right ? cur - 1 : cur + 1;
+        state = kFromSibling;
+      } else {
+        cur = link & 0xffff;
+      }
+      continue;
+    }
+    bool descend = false;
+    if ((link >> 21) & 1) {  // a leaf: its sphere
+      float t;
+      if (sphere_root(o, d, tmin, mk(A.x, A.y, A.z), B.x, t)) accept(t, __float_as_int(B.y));
+    } else {
+      const float x0 = (A.x - o.x) * ix, x1 = (B.x - o.x) * ix;
+      const float y0 = (A.y - o.y) * iy, y1 = (B.y - o.y) * iy;
+      const float z0 = (A.z - o.z) * iz, z1 = (B.z - o.z) * iz;
+      const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+      const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+      const float slack = 1e-5f * fabsf(tf) + 1e-7f;
+      descend = tn <= tf + slack && tf >= 0.0f && tn <= h.t * 1.00001f + 1e-7f;
+    }
+    if (descend) {
+      cur = left + (int)((neg >> ((link >> 16) & 3)) & 1u);
+      state = kFromParent;
+    } else if (cur == 0) {
+      break;  // the root itself missed (or is the only leaf)
+    } else if (state == kFromParent) {
+      cur = right ? cur - 1 : cur + 1;
+      state = kFromSibling;
+    } else {
+      cur = link & 0xffff;
+      state = kFromChild;
+    }
+  }
+}
+
 // qshade: the block's LDS copy of the quads' shading data (n, alb, mt) so
 // the hit's material is an LDS gather instead of a global one.
 // Every quad of a scene (kMaxQuads, 8 KiB): with a table that could be
@@ -342,9 +412,9 @@ RTP_DEV bool quad_hit_axis(const PreExact& E, f3 o, f3 d, float& t_out) {
   return ok1 & !(second & bad2);
 }
 
-template <bool kBvh>
+template <bool kBvh, bool kLdsBvh = false>
 RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefilter,
-                        uint32_t* full_out, const float* lds_prex) {
+                        uint32_t* full_out, const float* lds_prex, const LdsBvhNode* lds_bvh = nullptr) {
   Hit h{3.40282347e+38f, -1, 0};
   const float tmin = 0.001f;
   // the (t, orig) key minimum: the order the kinds are scanned in is free
@@ -411,7 +481,9 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
     h.idx = (int)(key & 0xffu);
   }
   static_assert(kQuadKinds == 11, "closest_hit scans every kind");
-  if constexpr (kBvh) {
+  if constexpr (kLdsBvh) {
+    spheres_bvh_lds(lds_bvh, o, d, h);
+  } else if constexpr (kBvh) {
     spheres_bvh(sc, o, d, h);
   } else {
     const int ns = sc->n_spheres;
@@ -460,9 +532,9 @@ RTP_DEV unsigned long long stamp(bool on) { return on ? __builtin_amdgcn_s_memti
 // depth-k draws (which + generator, exactly one dead step) to the caller's
 // fast-forward instead of drawing them here.
 // qshade: the block's LDS quad table (fill_qshade).
-template <bool kBvh, bool kDeferDead = false>
+template <bool kBvh, bool kDeferDead = false, bool kLdsBvh = false>
 RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3& emit, float4* __restrict__ hist_d,
-                   int D, unsigned long long* dbg, const float* qshade) {
+                   int D, unsigned long long* dbg, const float* qshade, const LdsBvhNode* lds_bvh = nullptr) {
   const bool st = dbg != nullptr;
   const unsigned long long t0 = stamp(st);
   const uint32_t t1 = sc->which_t1, t2 = sc->which_t2;
@@ -471,7 +543,7 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
   const int d = ps.d;
   // intersect + CollectIntersecttWorklet (SurfaceWorklets.h:104-109)
   uint32_t fb = 0;  // (stats) 1: this lane ran the exact scan of the prefiltered quads
-  Hit h = closest_hit<kBvh>(sc, org, dir, true, st ? &fb : nullptr, qshade + kPrexLdsOffset);
+  Hit h = closest_hit<kBvh, kLdsBvh>(sc, org, dir, true, st ? &fb : nullptr, qshade + kPrexLdsOffset, lds_bvh);
   if (st) {
     const unsigned long long m = __ballot(fb == 1u);
     dbg[kDbgFallbackSteps] += m ? 1 : 0;
@@ -789,20 +861,22 @@ typedef const __attribute__((address_space(1))) uint32_t GU32;
 // kPlan: a planned launch (KParams::wave_begin): wave w owns the entries
 // [wave_begin[w], wave_begin[w+1]) -- up to kPool of them, grouped by their
 // expected cost -- instead of the interleaved entries j * n_waves + w.
-template <bool kStats, bool kBvh, bool kTiles = false, bool kPlan = false>
-#if RTP_POOL_MAX_VGPR > 0
-#define RTP_POOL_VGPR_ATTR __attribute__((amdgpu_num_vgpr(RTP_POOL_MAX_VGPR)))
-#else
-#define RTP_POOL_VGPR_ATTR
-#endif
-__global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_ATTR rtp_render_pool(const DevScene* __restrict__ sc, KParams p, int n_waves) {
-  __shared__ __align__(16) unsigned char smem[kPoolLdsBytes];
-  __shared__ __align__(16) float s_qshade[kQTableFloats];
+// The pool kernel's body; kWPB waves per block, kLdsBvh: the sphere BVH is
+// walked out of the block's LDS copy (s_bvh, rtp_render_pool_lds).
+template <bool kStats, bool kBvh, bool kTiles, bool kPlan, int kWPB, bool kLdsBvh>
+__device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const KParams& p, int n_waves,
+                                          unsigned char* smem, float* s_qshade, LdsBvhNode* s_bvh) {
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
-  const int w = blockIdx.x * kWavesPerBlock + wib;  // global wave id
+  const int w = blockIdx.x * kWPB + wib;  // global wave id
   // the quads' shading data into LDS (the block's only barrier, before any wave leaves)
   fill_qshade(sc, s_qshade);  // (n_quads <= kMaxQuads = kLdsQuads)
+  if constexpr (kLdsBvh) {    // and the sphere BVH (n_lnodes <= kLdsBvhMaxNodes, checked on the host)
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const auto* src = (const __attribute__((address_space(1))) f4v*)sc->lnodes;
+    f4v* dst = reinterpret_cast<f4v*>(s_bvh);
+    for (int i = threadIdx.x; i < 2 * sc->n_lnodes; i += blockDim.x) dst[i] = src[i];
+  }
   __syncthreads();
   if (w >= n_waves) return;  // whole wave leaves; no block-level barriers follow
   unsigned char* base = smem + (size_t)wib * kPool * kSlotBytes;
@@ -1041,8 +1115,8 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
     unsigned long long tbnc = ta;
     if (has_path) {
       f3 emit = mk(0.f, 0.f, 0.f);
-      const int res = bounce<kBvh, true>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D, want_dbg ? dbg : nullptr,
-                                         s_qshade);
+      const int res = bounce<kBvh, true, kLdsBvh>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D,
+                                                  want_dbg ? dbg : nullptr, s_qshade, s_bvh);
       tbnc = stamp(want_dbg);
       if (res == kAlive && ps.d < D - 1) {
         ps.d++;
@@ -1118,6 +1192,35 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
     if (p.live_out) p.live_out[k] = s_live[j];
   }
 }
+
+#if RTP_POOL_MAX_VGPR > 0
+#define RTP_POOL_VGPR_ATTR __attribute__((amdgpu_num_vgpr(RTP_POOL_MAX_VGPR)))
+#else
+#define RTP_POOL_VGPR_ATTR
+#endif
+template <bool kStats, bool kBvh, bool kTiles = false, bool kPlan = false>
+__global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_ATTR
+    rtp_render_pool(const DevScene* __restrict__ sc, KParams p, int n_waves) {
+  __shared__ __align__(16) unsigned char smem[kPoolLdsBytes];
+  __shared__ __align__(16) float s_qshade[kQTableFloats];
+  pool_body<kStats, kBvh, kTiles, kPlan, kWavesPerBlock, false>(sc, p, n_waves, smem, s_qshade, nullptr);
+}
+
+// Scenes whose sphere BVH fits the LDS (LdsBvhNode, <= kLdsBvhMaxNodes):
+// one 16-wave block per CU (4 waves per SIMD, <= 128 VGPRs) shares one LDS
+// copy of the tree -- dynamic LDS after the waves' pools and the quad tables.
+template <bool kTiles>
+__global__ void __launch_bounds__(64 * kLdsBvhWavesPerBlock, 1) __attribute__((amdgpu_num_vgpr(128)))
+    rtp_render_pool_lds(const DevScene* __restrict__ sc, KParams p, int n_waves) {
+  __shared__ __align__(16) unsigned char smem[kLdsBvhWavesPerBlock * kPool * kSlotBytes];
+  __shared__ __align__(16) float s_qshade[kQTableFloats];
+  extern __shared__ __align__(16) unsigned char s_dyn[];
+  pool_body<false, true, kTiles, false, kLdsBvhWavesPerBlock, true>(sc, p, n_waves, smem, s_qshade,
+                                                                    reinterpret_cast<LdsBvhNode*>(s_dyn));
+}
+constexpr int kLdsBvhStaticBytes = kLdsBvhWavesPerBlock * kPool * kSlotBytes + kQTableFloats * 4;
+static_assert(kLdsBvhStaticBytes + kLdsBvhMaxNodes * (int)sizeof(LdsBvhNode) <= 160 * 1024,
+              "the LDS walk's block fits the CU's 160 KiB");
 
 // ------------------------------------------------------- diagnostics ---
 __global__ void rtp_eval_primitive_kernel(int kind, const void* in, void* out, int64_t n, const uint32_t* tab,
@@ -1228,13 +1331,30 @@ int resident_blocks_per_cu() {
     nb = 1;
   return nb;
 }
-int pool_resident_waves(bool stats, bool bvh) {
-  static int cached[2][2] = {{-1, -1}, {-1, -1}};
+int lds_bvh_resident_blocks_per_cu() {
+  const int dyn = rtp::kLdsBvhMaxNodes * (int)sizeof(rtp::LdsBvhNode);
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rtp::rtp_render_pool_lds<false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rtp::rtp_render_pool_lds<true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtp::rtp_render_pool_lds<false>,
+                                                   64 * rtp::kLdsBvhWavesPerBlock, dyn) != hipSuccess || nb <= 0)
+    nb = 1;
+  return nb;
+}
+// bvh: 0 no sphere BVH, 1 the global threaded walk, 2 the LDS walk
+int pool_resident_waves(bool stats, int bvh) {
+  static int cached[2][3] = {{-1, -1, -1}, {-1, -1, -1}};
   int& c = cached[stats][bvh];
   if (c > 0) return c;
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 1024;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  if (bvh == 2) {
+    c = cus * lds_bvh_resident_blocks_per_cu() * rtp::kLdsBvhWavesPerBlock;
+    return c;
+  }
   const int nb = stats ? (bvh ? resident_blocks_per_cu<true, true>() : resident_blocks_per_cu<true, false>())
                        : (bvh ? resident_blocks_per_cu<false, true>() : resident_blocks_per_cu<false, false>());
   c = cus * nb * rtp::kWavesPerBlock;
@@ -1272,7 +1392,7 @@ extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int bvh, int* variant_ou
   const int64_t by_lanes = (npix + wave_px - 1) / wave_px;
   const int64_t by_pool = (npix + rtp::kPool - 1) / rtp::kPool;
   const char* st = getenv("RTP_DEBUG_STATS");
-  int64_t W = std::min<int64_t>(by_lanes, pool_resident_waves(st && st[0] == '1', bvh != 0));
+  int64_t W = std::min<int64_t>(by_lanes, pool_resident_waves(st && st[0] == '1', bvh));
   W = std::max<int64_t>(W, by_pool);
   W = std::max<int64_t>(W, 1);
   if (waves_out) *waves_out = (int)W;
@@ -1288,7 +1408,7 @@ extern "C" hipError_t rtp_launch_eval_closest(const rtp::DevScene* scene, const 
   return hipGetLastError();
 }
 extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::KParams* p, int variant, int waves,
-                                        int bvh, hipStream_t stream) {
+                                        int bvh, hipStream_t stream, int n_lnodes) {
   if (p->npix <= 0) return hipSuccess;
   if (variant == 1 && p->tile_world > 0) return hipErrorNotSupported;  // (v1 takes pixel lists or ranges)
   if (variant == 1) {
@@ -1297,6 +1417,14 @@ extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::K
       hipLaunchKernelGGL(rtp::rtp_render_lockstep<true>, dim3((unsigned)grid), dim3(256), 0, stream, scene, *p);
     else
       hipLaunchKernelGGL(rtp::rtp_render_lockstep<false>, dim3((unsigned)grid), dim3(256), 0, stream, scene, *p);
+  } else if (bvh == 2) {  // the sphere BVH walked out of LDS
+    if (p->wave_begin || n_lnodes <= 0 || n_lnodes > rtp::kLdsBvhMaxNodes) return hipErrorNotSupported;
+    (void)lds_bvh_resident_blocks_per_cu();  // (sets the kernels' dynamic-LDS limit once)
+    const int blocks = (waves + rtp::kLdsBvhWavesPerBlock - 1) / rtp::kLdsBvhWavesPerBlock;
+    const dim3 g((unsigned)blocks), b(64 * rtp::kLdsBvhWavesPerBlock);
+    const size_t dyn = (size_t)n_lnodes * sizeof(rtp::LdsBvhNode);
+    if (p->tile_world > 0) hipLaunchKernelGGL(rtp::rtp_render_pool_lds<true>, g, b, dyn, stream, scene, *p, waves);
+    else hipLaunchKernelGGL(rtp::rtp_render_pool_lds<false>, g, b, dyn, stream, scene, *p, waves);
   } else {
     const int blocks = (waves + rtp::kWavesPerBlock - 1) / rtp::kWavesPerBlock;
     const char* st = getenv("RTP_DEBUG_STATS");

@@ -110,6 +110,23 @@ constexpr int32_t kBvhLeafSphere = -1;
 #define RTP_BVH_EMBED 1
 #endif
 
+// The same SAH tree for a walk out of LDS (rtp_kernels.hip spheres_bvh_lds):
+// ONE copy for every ray direction, the two children of an inner node
+// adjacent (left at an odd index L, right at L + 1; root 0), and every node
+// knowing its parent, its own split axis, its parent's split axis and which
+// child it is, so the walk needs neither a stack nor per-octant copies
+// (stackless traversal with parent links, Hapala et al. 2011).  Leaves hold
+// their one sphere: a = centre, b[0] = radius^2, b[1] = sphere index.
+struct alignas(16) LdsBvhNode {
+  float a[3];     // inner: box lo (padded as BvhNode's); leaf: sphere centre
+  int32_t link;   // parent (bits 0-15) | own axis << 16 | parent axis << 18 | right child << 20 | leaf << 21
+  float b[3];     // inner: box hi; leaf: r^2, sphere index (int bits), 0
+  int32_t left;   // inner: left child (right = left + 1); leaf: -1
+};
+static_assert(sizeof(LdsBvhNode) == 32, "two 16-byte LDS reads per node");
+constexpr int kLdsBvhMaxNodes = 2816;  // 88 KiB of dynamic LDS beside the 16-wave block's pools and tables
+constexpr int kLdsBvhWavesPerBlock = 16;
+
 struct alignas(16) DevLights {
   DevQuad quad;   // light quad for QuadPDFWorklet (PdfWorklet.h:230-248)
   float area;     // Magnitude(r-q) * Magnitude(t-q)
@@ -158,7 +175,8 @@ struct alignas(16) DevScene {
   uint32_t which_t2;  // smallest hash with which == 3
   float ior;
   int32_t n_nodes;                 // BVH scenes (n_spheres >= kBvhMinSpheres): nodes per octant copy
-  int32_t pad[3];
+  int32_t n_lnodes;                // LDS walk: nodes of lnodes (0: none)
+  int32_t pad[2];
   const BvhNode* nodes;            // 8 * n_nodes: one threaded copy per ray-direction octant
   const DevSphereG* sph_geom;      // BVH leaf order
   const DevSphere* sph_all;        // scene order (materials of the hit sphere)
@@ -174,6 +192,8 @@ struct alignas(16) DevScene {
   int32_t pad2[2];
   PreQuad pre[kMaxPre];
   PreExact prex[kMaxPre];  // by quad position (< n_pre)
+  const LdsBvhNode* lnodes;  // the LDS walk's tree (global copy, loaded per block; n_lnodes above)
+  const void* pad_ptr;
 };
 // The pool kernel's scans prefetch up to two records past the last quad or
 // prefilter record; these must stay inside DevScene (values never used).

@@ -100,3 +100,56 @@ def test_gpu_lbvh_c3_golden(rtp, device, monkeypatch):
     got = device.render_pixels(rtp.default_camera(), int(g["nx"]), int(g["ny"]), int(g["spp"]), int(g["depth"]), pix)
     want = (np.concatenate([g["rgb"][:256], np.zeros((256, 1), np.float32)], 1), g["final_seed"][:256], g["live"][:256])
     assert_render_equal(got[:3], want, "C3 golden, gpu-built BVH")
+
+
+def _oracle_scene(oracle, n, seed):
+    sc, pts, c, r, mat, tex = _random_sphere_scene(oracle, n, seed)
+    k0 = 6 * 4
+    for i, (ci, ri, mi, ti) in enumerate(zip(c, r, mat, tex)):
+        sc.points[k0 + i][:] = [float(v) for v in ci]
+        sc.sphere_point[i] = k0 + i
+        sc.sphere_radius[i] = float(ri)
+        sc.sphere_mat[i] = int(mi)
+        sc.sphere_tex[i] = int(ti)
+    sc.n_points = k0 + len(c)
+    sc.n_spheres = len(c)
+    sc.light_sphere_point = k0
+    return sc
+
+
+def test_lds_walk_matches_oracle_1200_spheres(rtp, oracle, device, monkeypatch):
+    """1200 spheres (2399 nodes: the tree fits the LDS walk, rtp_render_pool_lds)
+    against the oracle's brute-force closest hit, bit-exact."""
+    sc = _oracle_scene(oracle, 1200, 21)
+    nx = ny = 256
+    pix = np.sort(np.random.default_rng(8).choice(nx * ny, 512, replace=False)).astype(np.int64)
+    want = oracle.render_pixels(sc, oracle.camera_setup(nx, ny), nx, ny, 8, 50, pix)
+    monkeypatch.setenv("RTP_BVH_BUILD", "host")
+    set_scene_from_oracle(device, sc)
+    assert_render_equal(_render(device, rtp, nx, ny, 8, 50, pix), want, "LDS walk, 1200 spheres")
+
+
+def test_lds_walk_equals_global_walk_c3(rtp, device, monkeypatch):
+    """The C3 scene through the LDS walk (default for its 1999-node tree) and
+    the global threaded walk (RTP_BVH_LDS=0), on a pixel list and through the
+    tile-deal instance: the same bits."""
+    import torch
+
+    from raytracingtherestofyourlife_amd import shard
+
+    nx = ny = 128
+    cam = rtp.default_camera()
+    ids = shard.tile_pixels(nx, ny, 1, 3)
+    out = {}
+    for mode in ("lds", "global"):
+        monkeypatch.setenv("RTP_BVH_LDS", "1" if mode == "lds" else "0")
+        device.set_cornell_box(3)
+        out[mode] = _render(device, rtp, nx, ny, 8, 50, ids)
+        t = torch.zeros((ids.size, 4), dtype=torch.float32, device="cuda")
+        device.render_tiles_device(cam, nx, ny, 8, 50, t.data_ptr(), 1, 3, timed=True)
+        out[mode + "_tiles"] = (t.cpu().numpy(), None, None)
+    monkeypatch.delenv("RTP_BVH_LDS")
+    device.set_cornell_box(0)
+    assert_render_equal(out["lds"], out["global"], "C3: LDS walk vs global walk")
+    assert_render_equal(out["lds_tiles"], out["lds"], "C3: LDS walk, tile-deal instance vs pixel list")
+    assert_render_equal(out["global_tiles"], out["global"], "C3: global walk, tile-deal instance vs pixel list")
