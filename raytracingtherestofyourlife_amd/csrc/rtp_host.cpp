@@ -752,8 +752,12 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     std::vector<int32_t> order;
     std::vector<TNode> tree;
     bvh_build(P, 0, s->n_spheres, tree, order);
+    // the LDS walk (rtp_render_pool_lds) is opt-in, RTP_BVH_LDS=1: on C3 it
+    // ran 1118 ms against the global threaded walk's 591 (32 spp, r03f):
+    // 48% more VALU instructions for the stackless state machine, and lanes
+    // diverge as much as on the global walk (13 vs 17 of 64 per instruction)
     const char* le = getenv("RTP_BVH_LDS");
-    if (!(le && le[0] == '0') && bvh_lds_layout(tree, order, sph, lnodes)) h->n_lnodes = (int32_t)lnodes.size();
+    if (le && le[0] == '1' && bvh_lds_layout(tree, order, sph, lnodes)) h->n_lnodes = (int32_t)lnodes.size();
     for (int oct = 0; oct < 8; oct++) {  // 8 copies of n_nodes entries, indices local to each copy
       std::vector<rtp::BvhNode> one;
       bvh_flatten(tree, 0, oct, order, sph, one);

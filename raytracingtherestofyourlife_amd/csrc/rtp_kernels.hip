@@ -39,9 +39,8 @@
 #ifndef RTP_FF_MARGIN
 #define RTP_FF_MARGIN 12  // pool kernel: fast-forward when READY holds fewer than idle lanes + this
 #endif
-#ifndef RTP_HIST_SLOT
-#define RTP_HIST_SLOT 0
-#endif
+// history rows of a finished sample loaded together in the fast-forward batch
+constexpr int kHistPrefetch = 6;
 #ifndef RTP_CRIT_FF
 #define RTP_CRIT_FF 100  // pool kernel: lag (per mille of the wave's average samples) that makes a pixel critical
 #endif
@@ -922,17 +921,11 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
   // attenuation history per pixel SLOT, D rows: a pixel has one sample in
   // flight, so its history survives until the fast-forward batch that
   // computes the sample's radiance (row k of a light hit holds E_k)
-#if RTP_HIST_SLOT
-  // slot-major [wave*kPool + slot][row], kHistRows rows per slot: a path's
-  // rows 0..7 share one 128-byte line
-  const int D8 = (D + 7) & ~7;
-  float4* __restrict__ const hist_base = reinterpret_cast<float4*>(p.hist) + (int64_t)w * kPool * D8;
-  const int64_t stride = 1, slot_stride = D8;
-#else
-  // depth-major [d][wave*kPool + slot]
+  // depth-major [d][wave*kPool + slot]: the hot depths 0..4 of all slots
+  // stay dense.  (A slot-major layout, one pixel's rows in one 128-byte line,
+  // measured no faster: r03c, profiles/r03c_ab_history_prex.txt.)
   float4* __restrict__ const hist_base = reinterpret_cast<float4*>(p.hist) + (int64_t)w * kPool;
-  const int64_t stride = (int64_t)n_waves * kPool, slot_stride = 1;
-#endif
+  const int64_t stride = (int64_t)n_waves * kPool;
   float4* __restrict__ hist = hist_base;  // per lane: hist_base + slot of its path
   const f3 eye = ld3(p.cam.eye);
 
@@ -999,12 +992,27 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
         f3 c;
         if (flags & kEndLight) {
           const int k_end = D - frem;  // a light hit ends the path: rem = D - 1 - k_end + 1
-          const float4* __restrict__ hp = hist_base + fslot * slot_stride;
-          const float4 e = hp[(int64_t)k_end * stride];
-          float sx = e.x + 0.0f, sy = e.y + 0.0f, sz = e.z + 0.0f;
-          // two history rows per trip, both loads in flight together; the
-          // products stay in the reference's order (depth k_end-1 down to 0)
-          int dd = k_end - 1;
+          const float4* __restrict__ hp = hist_base + fslot;
+          // rows k_end (E) and k_end-1 .. k_end-5 issued together (clamped to
+          // row 0; rows below 0 are not applied), the rest two per trip;
+          // products in the reference's order (depth k_end-1 down to 0).
+          // One wait instead of up to three dependent round trips: C2 -1%
+          // (r03f, profiles/r03f_ab_history_prefetch.txt).
+          f3 rw[kHistPrefetch];
+#pragma unroll
+          for (int i = 0; i < kHistPrefetch; i++) {
+            const float4 v = hp[(int64_t)max(k_end - i, 0) * stride];
+            rw[i] = mk(v.x, v.y, v.z);
+          }
+          float sx = rw[0].x + 0.0f, sy = rw[0].y + 0.0f, sz = rw[0].z + 0.0f;
+#pragma unroll
+          for (int i = 1; i < kHistPrefetch; i++) {
+            const bool on = k_end - i >= 0;
+            sx = on ? 0.0f + rw[i].x * sx : sx;
+            sy = on ? 0.0f + rw[i].y * sy : sy;
+            sz = on ? 0.0f + rw[i].z * sz : sz;
+          }
+          int dd = k_end - kHistPrefetch;
           for (; dd >= 1; dd -= 2) {
             const float4 a = hp[(int64_t)dd * stride], b = hp[(int64_t)(dd - 1) * stride];
             sx = 0.0f + a.x * sx;
@@ -1091,7 +1099,7 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
       if (r < take) {
         slot = q_ready[(ready_head + r) & (kPool - 1)];
         seed = s_seed[slot];
-        hist = hist_base + slot * slot_stride;
+        hist = hist_base + slot;
         // the camera and tile constants re-read from the kernel arguments
         // here (kparams): kept live through the loop they were SGPRs spilled
         // to VGPR lanes, ~30 v_readlane per refill (through the kernarg

@@ -125,14 +125,17 @@ def test_lds_walk_matches_oracle_1200_spheres(rtp, oracle, device, monkeypatch):
     pix = np.sort(np.random.default_rng(8).choice(nx * ny, 512, replace=False)).astype(np.int64)
     want = oracle.render_pixels(sc, oracle.camera_setup(nx, ny), nx, ny, 8, 50, pix)
     monkeypatch.setenv("RTP_BVH_BUILD", "host")
+    monkeypatch.setenv("RTP_BVH_LDS", "1")  # (opt-in: slower than the global walk on C3)
     set_scene_from_oracle(device, sc)
     assert_render_equal(_render(device, rtp, nx, ny, 8, 50, pix), want, "LDS walk, 1200 spheres")
+    monkeypatch.delenv("RTP_BVH_LDS")
+    device.set_cornell_box(0)
 
 
 def test_lds_walk_equals_global_walk_c3(rtp, device, monkeypatch):
-    """The C3 scene through the LDS walk (default for its 1999-node tree) and
-    the global threaded walk (RTP_BVH_LDS=0), on a pixel list and through the
-    tile-deal instance: the same bits."""
+    """The C3 scene through the LDS walk (RTP_BVH_LDS=1, its 1999-node tree
+    fits) and the global threaded walk (the default), on a pixel list and
+    through the tile-deal instance: the same bits."""
     import torch
 
     from raytracingtherestofyourlife_amd import shard
