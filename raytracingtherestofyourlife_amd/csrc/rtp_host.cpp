@@ -908,7 +908,7 @@ rtp_status check_render_args(rtp_context* c, const rtp_camera* cam, int32_t nx, 
   // device-side bookkeeping limits: the pool kernel packs the remaining dead
   // depths into 14 bits and counts a wave's finished samples (<= 256 * spp)
   // in 32-bit signed cursors
-  if (depth > rtp::kMaxDepth) return fail(RTP_ERR_INVALID_ARGUMENT, "render: depthcount must be <= 16383");
+  if (depth > rtp::kMaxDepth) return fail(RTP_ERR_INVALID_ARGUMENT, "render: depthcount must be <= 8191");
   if (spp > rtp::kMaxSpp) return fail(RTP_ERR_INVALID_ARGUMENT, "render: samplecount must be <= 8388607");
   return RTP_OK;
 }

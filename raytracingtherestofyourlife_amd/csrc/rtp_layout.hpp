@@ -12,7 +12,7 @@
 namespace rtp {
 
 constexpr int kMaxQuads = 256;
-constexpr int kMaxDepth = 16383;    // remaining dead depths fit the 14-bit field of the pool's slots
+constexpr int kMaxDepth = 8191;     // remaining dead depths fit the 13-bit field of the pool's slots
 constexpr int kMaxSpp = 8388607;    // 256 slots * spp fits the pool's 32-bit sample cursors
 constexpr int kMaxSpheres = 256;          // held inline in DevScene (scalar loads)
 constexpr int kMaxSpheresBvh = 1 << 22;   // spheres behind the BVH (global memory)

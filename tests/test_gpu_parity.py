@@ -216,7 +216,7 @@ def test_invalid_arguments(device, rtp):
     with pytest.raises(rtp.RtpError):
         device.render_pixels(cam, 4, 4, 1, 1, np.array([16], dtype=np.int64))
     with pytest.raises(rtp.RtpError):  # device bookkeeping limits (rtp_layout.hpp kMaxDepth / kMaxSpp)
-        device.render(cam, 4, 4, 1, 16384)
+        device.render(cam, 4, 4, 1, 8192)
     with pytest.raises(rtp.RtpError):
         device.render(cam, 4, 4, 8388608, 1)
 

@@ -44,3 +44,23 @@ def test_gpu_tile_deal_rejects_partial_tiles(device):
         device.render_tiles_device(rtp.default_camera(), 40, 32, 1, 5, out.data_ptr(), 0, 1)
     with pytest.raises(Exception):
         device.render_tiles_device(rtp.default_camera(), 32, 32, 1, 5, out.data_ptr(), 2, 2)
+
+
+def test_launch_rejects_more_than_int32_entries(device):
+    """The kernels index a launch's entries with 32-bit integers: a pixel list
+    of 2^31 entries is refused before any allocation (rtp_host.cpp launch)."""
+    import ctypes
+
+    import raytracingtherestofyourlife_amd as rtp
+    from raytracingtherestofyourlife_amd._lib import RtpPixelAux, check
+
+    device.set_cornell_box(0)
+    cam = rtp.default_camera().to_c()
+    L = rtp.load()
+    st = L.rtp_render_device(device.handle, ctypes.byref(cam), 800, 800, 1, 5, 0, 0, 1 << 31,
+                             ctypes.c_void_p(0x1000), ctypes.c_void_p(0x2000), ctypes.byref(RtpPixelAux()),
+                             ctypes.c_void_p(None), None)
+    assert st == rtp._lib.RTP_ERR_INVALID_ARGUMENT
+    assert "2^31" in L.rtp_last_error().decode()
+    with pytest.raises(rtp.RtpError):
+        check(st)

@@ -37,6 +37,7 @@ ap.add_argument("--rank", type=int, default=0)
 ap.add_argument("--pre-spp", type=int, default=16)
 ap.add_argument("--ff", type=float, default=1.0, help="per-sample overhead in bounce steps (fast-forward, refill)")
 ap.add_argument("--resident", type=int, default=5120)
+ap.add_argument("--cap", type=int, default=128, help="most pixels per wave (64: grouping only, no packing)")
 ap.add_argument("--reps", type=int, default=3)
 a = ap.parse_args()
 
@@ -63,12 +64,12 @@ def plan(cost):
     order = np.argsort(-cost, kind="stable")
     c = cost[order]
     T = max(c.max(), c.sum() / (64 * a.resident))
-    w = np.maximum(c / (64 * T), 1 / 127.5)
+    w = np.maximum(c / (64 * T), 1 / (a.cap - 0.5))
     start = np.concatenate([[0.0], np.cumsum(w)[:-1]])
     wid = np.floor(start).astype(np.int64)
     nw = int(wid[-1]) + 1
     wb = np.searchsorted(wid, np.arange(nw + 1), side="left").astype(np.int32)
-    assert wb[-1] == n and (np.diff(wb) <= 128).all() and (np.diff(wb) > 0).all()
+    assert wb[-1] == n and (np.diff(wb) <= a.cap).all() and (np.diff(wb) > 0).all()
     return order, wb, T
 
 
