@@ -41,9 +41,6 @@
 #endif
 // history rows of a finished sample loaded together in the fast-forward batch
 constexpr int kHistPrefetch = 6;
-#ifndef RTP_SPEC_FF
-#define RTP_SPEC_FF 0
-#endif
 #ifndef RTP_CRIT_FF
 #define RTP_CRIT_FF 100  // pool kernel: lag (per mille of the wave's average samples) that makes a pixel critical
 #endif
@@ -534,16 +531,9 @@ RTP_DEV unsigned long long stamp(bool on) { return on ? __builtin_amdgcn_s_memti
 // depth-k draws (which + generator, exactly one dead step) to the caller's
 // fast-forward instead of drawing them here.
 // qshade: the block's LDS quad table (fill_qshade).
-// The state after a dying path's remaining dead depths from the direct jump
-// table of their count, issued where the death is known (a miss, or a light
-// hit), so the read's latency hides behind the rest of the wave's bounce
-// (RTP_SPEC_FF); *ok = false when no direct table covers the count.
-RTP_DEV uint32_t ff_at_death(uint32_t seed, int rem, bool* ok);
-
 template <bool kBvh, bool kDeferDead = false, bool kLdsBvh = false>
 RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3& emit, float4* __restrict__ hist_d,
-                   int D, unsigned long long* dbg, const float* qshade, const LdsBvhNode* lds_bvh = nullptr,
-                   uint32_t* ff_state = nullptr, bool* ff_ok = nullptr) {
+                   int D, unsigned long long* dbg, const float* qshade, const LdsBvhNode* lds_bvh = nullptr) {
   const bool st = dbg != nullptr;
   const unsigned long long t0 = stamp(st);
   const uint32_t t1 = sc->which_t1, t2 = sc->which_t2;
@@ -564,7 +554,6 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
   }
   if (h.kind < 0) {
     if (!kDeferDead) seed = dead_step(seed, t1, t2);  // which + generator draws of the now-dead ray
-    if (kDeferDead && ff_state) *ff_state = ff_at_death(seed, D - d, ff_ok);
     return kMissed;
   }
   f3 hp = add(org, scl(dir, h.t));
@@ -590,7 +579,6 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
   if (mt == 1) {  // DiffuseLightWorklet: emit, path ends (status &= 0)
     emit = (dot(hn, dir) < 0.0f) ? alb : mk(0.f, 0.f, 0.f);
     if (!kDeferDead) seed = dead_step(seed, t1, t2);
-    if (kDeferDead && ff_state) *ff_state = ff_at_death(seed, D - d, ff_ok);
     return kLight;
   }
   f3 atten;
@@ -807,11 +795,8 @@ static_assert((kPool & (kPool - 1)) == 0 && kPool >= 64, "pool size must be a po
 // 128 slots at 6 waves (80 VGPRs, spills) were slower.
 constexpr int kSlotBytes = 6 * 4 + 3 * 2;
 // s_rem packs the remaining dead depths with how the sample's path ended
-constexpr int kRemMask = 0x1fff, kEndFf = 0x2000, kEndLight = 0x4000, kEndNonfinite = 0x8000;
+constexpr int kRemMask = 0x3fff, kEndLight = 0x4000, kEndNonfinite = 0x8000;
 static_assert(kMaxDepth <= kRemMask, "the remaining dead depths fit s_rem's count field");
-// kEndFf: the dead depths were already skipped at the path's death (the
-// direct table read issued in bounce(), RTP_SPEC_FF): the batch only banks
-// the radiance and requeues the pixel
 constexpr int kPoolLdsBytes = kWavesPerBlock * kPool * kSlotBytes;
 
 RTP_DEV uint32_t lane_rank(uint64_t mask) {  // number of set mask bits below this lane
@@ -873,14 +858,6 @@ RTP_DEV CKP& kparams() {
   return *pp;
 }
 typedef const __attribute__((address_space(1))) uint32_t GU32;
-RTP_DEV uint32_t ff_at_death(uint32_t seed, int rem, bool* ok) {
-  CKP& FP = kparams();
-  const bool hit = FP.ffd != nullptr && (unsigned)(rem - FP.ffd_first) < (unsigned)FP.ffd_count;
-  *ok = hit;
-  uint32_t v = seed;
-  if (hit) v = ((GU32*)(FP.ffd + ((uint64_t)(rem - FP.ffd_first) << 32)))[seed];
-  return v;
-}
 // kPlan: a planned launch (KParams::wave_begin): wave w owns the entries
 // [wave_begin[w], wave_begin[w+1]) -- up to kPool of them, grouped by their
 // expected cost -- instead of the interleaved entries j * n_waves + w.
@@ -1000,8 +977,7 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
       // remaining count when there is one (then it is the only read), else
       // the 32-depth table
       uint32_t early = 0;
-      const bool ff_done = (frem & kEndFf) != 0;  // skipped at the death: bank and requeue only
-      const int frc = ff_done ? 0 : frem & kRemMask;
+      const int frc = frem & kRemMask;
       CKP& FP = kparams();
       const bool has_direct = mine && FP.ffd != nullptr && (unsigned)(frc - FP.ffd_first) < (unsigned)FP.ffd_count;
       const bool has_early = mine && !has_direct && FP.ff[0] != nullptr && frc >= 32;
@@ -1062,7 +1038,6 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
         s_g[fslot] = s_g[fslot] + c.y;
         s_b[fslot] = s_b[fslot] + c.z;
       }
-      if (ff_done) frem = 0;
       // jump over 32 / 16 / 8 / 4 dead depths with one table read each
       // (HBM-resident tables of the dead-step map, built once per device),
       // then hash the few remaining depths
@@ -1149,11 +1124,8 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
     unsigned long long tbnc = ta;
     if (has_path) {
       f3 emit = mk(0.f, 0.f, 0.f);
-      uint32_t ff_state = 0;
-      bool ff_ok = false;
       const int res = bounce<kBvh, true, kLdsBvh>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D,
-                                                  want_dbg ? dbg : nullptr, s_qshade, s_bvh,
-                                                  RTP_SPEC_FF ? &ff_state : nullptr, &ff_ok);
+                                                  want_dbg ? dbg : nullptr, s_qshade, s_bvh);
       tbnc = stamp(want_dbg);
       if (res == kAlive && ps.d < D - 1) {
         ps.d++;
@@ -1164,10 +1136,7 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
         // dead depths left: D-1-k_end, plus depth k_end's own draws when the
         // path died there (bounce<.., true> left them to the fast-forward)
         const int rem = D - 1 - k_end + (res != kAlive ? 1 : 0);
-        const bool spec = RTP_SPEC_FF && res != kAlive && ff_ok;  // dead depths already skipped
-        if (spec) seed = ff_state;
-        s_rem[slot] = (uint16_t)(rem | (spec ? kEndFf : 0) | (res == kLight ? kEndLight : 0) |
-                                 (ps.nonfinite ? kEndNonfinite : 0));
+        s_rem[slot] = (uint16_t)(rem | (res == kLight ? kEndLight : 0) | (ps.nonfinite ? kEndNonfinite : 0));
         s_samples[slot] = s_samples[slot] + 1u;
         s_live[slot] = s_live[slot] + (uint32_t)(k_end + 1);
         s_seed[slot] = seed;
