@@ -196,7 +196,11 @@ def main() -> None:
     ids_np = shard.tile_pixels(nx, ny, rank, world)
     npix = ids_np.size
     # setup, timed: the context, the scene, the RNG jump tables (policy), then
-    # the first render -- what a fresh process pays before its first frame
+    # the first render -- what a fresh process pays before its first frame.
+    # The HIP runtime's own first-use initialisation (~120 ms on the first
+    # host-to-device copy of the process, r03j tools/scene_cost.py) is process
+    # start, like the imports: one small copy takes it before the timer.
+    torch.ones(1).cuda()
     torch.cuda.synchronize()
     t_setup = time.perf_counter()
     dev = rtp.Device(gpu)

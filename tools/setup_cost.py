@@ -30,6 +30,10 @@ ap.add_argument("--rank", type=int, default=0)
 ap.add_argument("--world", type=int, default=1)
 ap.add_argument("--ff-tables", default="auto", choices=["on", "auto", "off"], help="RNG jump-table policy")
 a = ap.parse_args()
+# the HIP runtime's first-use initialisation (first host-to-device copy) is
+# process start, as in bench.py
+torch.ones(1).cuda()
+torch.cuda.synchronize()
 t_import = time.perf_counter() - t_start
 
 t = time.perf_counter()
