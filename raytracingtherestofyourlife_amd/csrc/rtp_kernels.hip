@@ -1394,10 +1394,19 @@ extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int bvh, int* variant_ou
     if (waves_out) *waves_out = (int)((npix + 63) / 64);
     return npix;
   }
-  // pixels per wave when the launch cannot fill every resident wave with 64
-  // (experiments: RTP_WAVE_PIXELS)
-  int wave_px = 64;
-  if (const char* e = getenv("RTP_WAVE_PIXELS")) wave_px = std::max(1, std::min(64, atoi(e)));
+  // pixels per wave when the launch cannot fill every resident wave: 80, so
+  // that a lane often serves two pixels (the cheap pixels fill the lanes the
+  // expensive ones' sample chains leave idle) while the waves per SIMD stay
+  // few (each step of a chain is faster).  Rank 0's share of the C2 frame
+  // under the N-rank tile deal, kernel ms (r03k/l, profiles/r03k_*):
+  //   px/wave:  64    80    96    112   128
+  //   N = 2:    95.5  83.6  86.5  79.0  88.7
+  //   N = 4:    74.0  64.4  65.1  69.0  73.8
+  //   N = 8:    58.7  58.6  59.2   --   65.0
+  // (non-monotone: which pixels share a wave decides its longest chain).
+  // RTP_WAVE_PIXELS overrides (experiments).
+  int wave_px = 80;
+  if (const char* e = getenv("RTP_WAVE_PIXELS")) wave_px = std::max(1, std::min(rtp::kPool, atoi(e)));
   const int64_t by_lanes = (npix + wave_px - 1) / wave_px;
   const int64_t by_pool = (npix + rtp::kPool - 1) / rtp::kPool;
   const char* st = getenv("RTP_DEBUG_STATS");
