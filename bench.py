@@ -380,7 +380,8 @@ def main() -> None:
             "first_render_ms": round(first_ms, 2),
             "one_shot": None if world > 1 else {
                 "note": "a fresh process rendering this frame once, like main.cc (its timer, :584-585, 661-663; "
-                        "process start and imports excluded): context + scene + jump-table policy + one render",
+                        "process start, imports and the HIP runtime's first-use initialisation excluded): "
+                        "context + scene + jump-table policy + one render",
                 "default_policy": {"policy": "auto (no tables for one frame)",
                                    "end_to_end_ms": round(setup_base_ms + off_ms, 1),
                                    "render_ms": round(off_ms, 1),
