@@ -1404,13 +1404,18 @@ extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int bvh, int* variant_ou
   //   N = 4:    74.0  64.4  65.1  69.0  73.8
   //   N = 8:    58.7  58.6  59.2   --   65.0
   // (non-monotone: which pixels share a wave decides its longest chain).
-  // RTP_WAVE_PIXELS overrides (experiments).
-  int wave_px = 80;
+  // Below a third of the resident waves at 64 pixels (C1, the 1/8 share)
+  // the steps already run at one wave's latency: fewer waves gain nothing,
+  // and a second pixel on a lane only lengthens its chain (C1: 0.70 -> 0.80
+  // ms at 80), so such launches keep 64.  RTP_WAVE_PIXELS overrides
+  // (experiments).
+  const char* st = getenv("RTP_DEBUG_STATS");
+  const int64_t resident = pool_resident_waves(st && st[0] == '1', bvh);
+  int wave_px = (npix + 63) / 64 * 3 < resident ? 64 : 80;
   if (const char* e = getenv("RTP_WAVE_PIXELS")) wave_px = std::max(1, std::min(rtp::kPool, atoi(e)));
   const int64_t by_lanes = (npix + wave_px - 1) / wave_px;
   const int64_t by_pool = (npix + rtp::kPool - 1) / rtp::kPool;
-  const char* st = getenv("RTP_DEBUG_STATS");
-  int64_t W = std::min<int64_t>(by_lanes, pool_resident_waves(st && st[0] == '1', bvh));
+  int64_t W = std::min<int64_t>(by_lanes, resident);
   W = std::max<int64_t>(W, by_pool);
   W = std::max<int64_t>(W, 1);
   if (waves_out) *waves_out = (int)W;

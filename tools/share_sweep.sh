@@ -1,10 +1,12 @@
 #!/bin/bash
 # Kernel time of one rank's share of the C2 frame under the strong-scaling
-# tile deal (rank 0 of N), for each RTP_WAVE_PIXELS value given.
+# tile deal (rank 0 of N), for each RTP_WAVE_PIXELS value given ("default":
+# the library's own choice).
 # usage: tools/share_sweep.sh "<worlds>" "<wave_pixels values>"
 for n in $1; do
   for wp in $2; do
-    ms=$(RTP_WAVE_PIXELS=$wp timeout -k 10 300 python3 tools/quick_bench.py --tiles --spp 1000 --world "$n" --rank 0 --reps 3 | python3 -c '
+    if [ "$wp" = default ]; then unset RTP_WAVE_PIXELS; else export RTP_WAVE_PIXELS=$wp; fi
+    ms=$(timeout -k 10 300 python3 tools/quick_bench.py --tiles --spp 1000 --world "$n" --rank 0 --reps 3 | python3 -c '
 import json,sys
 print(min(json.loads(l)["kernel_ms"] for l in sys.stdin if l.startswith("{")))') || exit 1
     echo "world $n wave_pixels $wp kernel_ms $ms"
