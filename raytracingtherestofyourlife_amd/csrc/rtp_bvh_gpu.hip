@@ -240,3 +240,58 @@ extern "C" hipError_t rtp_build_bvh_gpu(const float4* d_cr, int n, float3 lo, fl
   cleanup();
   return hipSuccess;
 }
+
+namespace rtp {
+namespace {
+// f32 -> f16 bits rounded outward: the nearest half, then stepped toward
+// -inf (down) or +inf (up) until its value (decoded by the same instruction
+// the walk uses) is on the right side of x; if that fails, an infinity.
+__device__ uint32_t half_outward(float x, bool up) {
+  uint32_t b = __builtin_bit_cast(uint16_t, (_Float16)x);
+  for (int i = 0; i < 4; i++) {
+    const float v = (float)__builtin_bit_cast(_Float16, (uint16_t)b);
+    if (up ? v >= x : v <= x) return b;
+    const bool neg = (b & 0x8000u) != 0, zero = (b & 0x7fffu) == 0;
+    if (zero) b = up ? 0x0001u : 0x8001u;
+    else if (up) b = neg ? b - 1 : b + 1;
+    else b = neg ? b + 1 : b - 1;
+  }
+  return up ? 0x7c00u : 0xfc00u;
+}
+__global__ void k_compact(const BvhNode* __restrict__ nodes, int64_t total, uint32_t* __restrict__ cn,
+                          int32_t* __restrict__ cidx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const BvhNode nd = nodes[i];
+  uint32_t w[4];
+  int32_t idx = -1;
+  if (nd.leaf == kBvhLeafSphere) {
+    w[0] = __float_as_uint(nd.lo[0]);
+    w[1] = __float_as_uint(nd.lo[1]);
+    w[2] = __float_as_uint(nd.lo[2]);
+    w[3] = __float_as_uint(nd.hi[0]) | kCBvhSphereBit;
+    idx = __float_as_int(nd.hi[1]);
+  } else {
+    w[0] = half_outward(nd.lo[0], false) | half_outward(nd.lo[1], false) << 16;
+    w[1] = half_outward(nd.lo[2], false) | half_outward(nd.hi[0], true) << 16;
+    w[2] = half_outward(nd.hi[1], true) | half_outward(nd.hi[2], true) << 16;
+    w[3] = nd.leaf == 0 ? (uint32_t)nd.skip : kCBvhLeafBit | (uint32_t)nd.leaf;
+  }
+  reinterpret_cast<uint4*>(cn)[i] = make_uint4(w[0], w[1], w[2], w[3]);
+  cidx[i] = idx;
+}
+}  // namespace
+}  // namespace rtp
+
+// The walks' compact copy (rtp_layout.hpp kCBvhSphereBit) of `total` BvhNode
+// entries (all 8 octant copies): cn gets 4 words per node, cidx one index.
+extern "C" hipError_t rtp_compact_bvh(const rtp::BvhNode* d_nodes, int64_t total, uint32_t* d_cn, int32_t* d_cidx,
+                                      hipStream_t stream) {
+  if (total <= 0) return hipSuccess;
+  const int tb = 256;
+  hipLaunchKernelGGL(rtp::k_compact, dim3((unsigned)((total + tb - 1) / tb)), dim3(tb), 0, stream, d_nodes, total,
+                     d_cn, d_cidx);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(stream);
+  return e;
+}

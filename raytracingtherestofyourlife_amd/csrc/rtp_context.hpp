@@ -21,6 +21,8 @@ struct rtp_context {
   unsigned long long* d_progress = nullptr;  // global finished-sample counter of the pool kernel
   // many-sphere scenes: threaded BVH + sphere records (rtp_layout.hpp)
   rtp::BvhNode* d_nodes = nullptr;
+  uint32_t* d_cnodes = nullptr;  // compact copy of d_nodes (the walks read it)
+  int32_t* d_cidx = nullptr;     // scene index of each compact sphere leaf
   rtp::DevSphereG* d_sph_geom = nullptr;
   rtp::DevSphere* d_sph_all = nullptr;
   rtp::LdsBvhNode* d_lnodes = nullptr;  // the LDS walk's copy of the tree (small BVH scenes)

@@ -29,6 +29,8 @@ extern "C" hipError_t rtp_launch_eval_primitive(int kind, const void* in, void* 
                                                 uint32_t t1, uint32_t t2, hipStream_t stream);
 extern "C" hipError_t rtp_launch_build_ff_tables(const rtp::FfBuildOut* out, int max_r, uint32_t t1, uint32_t t2,
                                                  hipStream_t stream);
+extern "C" hipError_t rtp_compact_bvh(const rtp::BvhNode* d_nodes, int64_t total, uint32_t* d_cn, int32_t* d_cidx,
+                                      hipStream_t stream);
 extern "C" hipError_t rtp_build_bvh_gpu(const float4* d_cr, int n, float3 lo, float3 ext, rtp::BvhNode* d_nodes,
                                         rtp::DevSphereG* d_geom, hipStream_t stream);
 extern "C" hipError_t rtp_launch_eval_closest(const rtp::DevScene* scene, const float* rays, uint32_t* out,
@@ -600,6 +602,8 @@ void rtp_destroy(rtp_context* c) {
   if (c->d_sph_geom) (void)hipFree(c->d_sph_geom);
   if (c->d_sph_all) (void)hipFree(c->d_sph_all);
   if (c->d_lnodes) (void)hipFree(c->d_lnodes);
+  if (c->d_cnodes) (void)hipFree(c->d_cnodes);
+  if (c->d_cidx) (void)hipFree(c->d_cidx);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->done) (void)hipEventDestroy(c->done);
@@ -811,7 +815,8 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     if (e == hipSuccess) e = hipEventSynchronize(c->done);
     c->pending = false;
   }
-  for (void** p : {(void**)&c->d_nodes, (void**)&c->d_sph_geom, (void**)&c->d_sph_all, (void**)&c->d_lnodes})
+  for (void** p : {(void**)&c->d_nodes, (void**)&c->d_sph_geom, (void**)&c->d_sph_all, (void**)&c->d_lnodes,
+                   (void**)&c->d_cnodes, (void**)&c->d_cidx})
     if (*p && e == hipSuccess) {
       e = hipFree(*p);
       *p = nullptr;
@@ -859,6 +864,14 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     h->sph_geom = c->d_sph_geom;
     h->sph_all = c->d_sph_all;
     h->lnodes = c->d_lnodes;
+  }
+  if (use_bvh && e == hipSuccess) {  // the walks' compact copy of the octant arrays
+    const int64_t total = (int64_t)8 * h->n_nodes;
+    e = hipMalloc(&c->d_cnodes, (size_t)total * 16);
+    if (e == hipSuccess) e = hipMalloc(&c->d_cidx, (size_t)total * sizeof(int32_t));
+    if (e == hipSuccess) e = rtp_compact_bvh(c->d_nodes, total, c->d_cnodes, c->d_cidx, nullptr);
+    h->cnodes = c->d_cnodes;
+    h->cidx = c->d_cidx;
   }
   if (e == hipSuccess) e = hipMemcpy(c->d_scene, h, sizeof(*h), hipMemcpyHostToDevice);
   c->n_lnodes = h->n_lnodes;

@@ -44,6 +44,11 @@ constexpr int kHistPrefetch = 6;
 // and the rest kHistChunk at a time (r03r: 4 rows per wait, -0.4% at N = 1,
 // -1.1% at the 1/8 share, against two per wait)
 constexpr int kHistChunk = 4;
+#ifndef RTP_WALK_DONE
+// pool kernel, sphere-BVH scenes: a loop iteration walks the BVH until this
+// many of the wave's paths have finished their walks (or all have)
+#define RTP_WALK_DONE 48
+#endif
 #ifndef RTP_CRIT_FF
 #define RTP_CRIT_FF 100  // pool kernel: lag (per mille of the wave's average samples) that makes a pixel critical
 #endif
@@ -135,67 +140,107 @@ RTP_DEV bool sphere_root(f3 o, f3 d, float tmin, f3 c, float rr, float& t_out) {
 // only cull (padded on the host; compared with slack here), so no sphere
 // whose root could win is skipped.  (Loading node i+1 while testing i was
 // faster with flat loads and 16% slower with global ones: DESIGN.md 4.1.)
-RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
-  const float tmin = 0.001f;
-  const float ix = __builtin_amdgcn_rcpf(fabsf(d.x) < 1e-20f ? copysignf(1e-20f, d.x) : d.x);
-  const float iy = __builtin_amdgcn_rcpf(fabsf(d.y) < 1e-20f ? copysignf(1e-20f, d.y) : d.y);
-  const float iz = __builtin_amdgcn_rcpf(fabsf(d.z) < 1e-20f ? copysignf(1e-20f, d.z) : d.z);
-  const int nn = sc->n_nodes;
-  // the copy of the tree ordered near-to-far for this ray's direction octant
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) f4v GF4;
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u4v GU4;
+typedef const __attribute__((address_space(1))) int32_t GI32;
+// 1/d per component for the slab tests (tiny components clamped)
+RTP_DEV float slab_rcp(float v) { return __builtin_amdgcn_rcpf(fabsf(v) < 1e-20f ? copysignf(1e-20f, v) : v); }
+// A ray's view of the sphere BVH: the compact copy of the tree ordered
+// near-to-far for its direction octant (rtp_layout.hpp kCBvhSphereBit) and
+// that copy's sphere-index table.  (Global, address space 1, pointers: through
+// the generic ones loaded from the scene the walk compiled to flat loads.)
+struct BvhRay {
+  GU4* nodes;
+  GI32* cidx;
+  float ix, iy, iz;
+};
+RTP_DEV BvhRay bvh_ray(const DevScene* __restrict__ sc, f3 d) {
   const int oct = (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0);
-  // global (address space 1) pointers: through the generic ones loaded from
-  // the scene the walk compiled to flat loads
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  typedef const __attribute__((address_space(1))) f4v GF4;
-  GF4* __restrict__ nodes_g = (GF4*)(sc->nodes + (int64_t)oct * nn);
-  GF4* __restrict__ geom_g = (GF4*)sc->sph_geom;  // DevSphereG: 2 x 16 B
-  struct {
-    GF4* p;
-    RTP_DEV float4 operator[](int i) const {
-      const f4v v = p[i];
-      return make_float4(v.x, v.y, v.z, v.w);
+  const int64_t base = (int64_t)oct * sc->n_nodes;
+  return BvhRay{(GU4*)(sc->cnodes + 4 * base), (GI32*)(sc->cidx + base), slab_rcp(d.x), slab_rcp(d.y), slab_rcp(d.z)};
+}
+// During a walk a sphere hit is h.kind == 2 with h.idx the leaf's node (the
+// sphere's scene index is cidx[node]); bvh_resolve turns it into kind 1 with
+// the scene index.  Kind 1 hits (multi-sphere leaves) carry the index.
+RTP_DEV int bvh_hit_index(const Hit& h, GI32* cidx) { return h.kind == 2 ? cidx[h.idx] : h.idx; }
+RTP_DEV void bvh_resolve(Hit& h, GI32* cidx) {
+  if (h.kind == 2) {
+    h.idx = cidx[h.idx];
+    h.kind = 1;
+  }
+}
+// the closest-sphere update: the (t, scene index) minimum, quads winning t ties
+RTP_DEV void bvh_accept_leaf(Hit& h, float t, int node, GI32* cidx) {
+  if (t < h.t) {
+    h.t = t;
+    h.kind = 2;
+    h.idx = node;
+  } else if (t == h.t && h.kind >= 1) {  // an exact tie between spheres (rare): the smaller scene index
+    if (cidx[node] < bvh_hit_index(h, cidx)) {
+      h.kind = 2;
+      h.idx = node;
     }
-  } nodes{nodes_g};
-  auto accept = [&](float t, int orig) {
-    if (t < h.t || (t == h.t && h.kind == 1 && orig < h.idx)) {
-      h.t = t;
-      h.kind = 1;
-      h.idx = orig;
-    }
-  };
-  int ni = 0;
-  float4 a = nodes[0], b = nodes[1];
-  while (ni < nn) {
-    const int skip = __float_as_int(a.w), leaf = __float_as_int(b.w);
-    int next;
-    if (leaf == kBvhLeafSphere) {  // one embedded sphere: a.xyz centre, b.x radius^2, b.y index
+  }
+}
+RTP_DEV void bvh_accept_orig(Hit& h, float t, int orig, GI32* cidx) {
+  if (t < h.t || (t == h.t && h.kind >= 1 && orig < bvh_hit_index(h, cidx))) {
+    h.t = t;
+    h.kind = 1;
+    h.idx = orig;
+  }
+}
+RTP_DEV float half_lo(uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v & 0xffffu)); }
+RTP_DEV float half_hi(uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v >> 16)); }
+// One node of the walk: node ni (its 16 bytes v) is tested against the ray
+// and the best hit so far; returns the next node (>= n_nodes: the walk is
+// done).  A sphere leaf runs the exact root test (no box); an inner node's
+// box (padded on the host, rounded outward to half precision, compared with
+// slack here) only culls.
+RTP_DEV int bvh_visit(GF4* __restrict__ geom_g, const BvhRay& R, f3 o, f3 d, u4v v, int ni, Hit& h) {
+  if ((int32_t)v.w < 0) {  // a sphere leaf: centre, r^2
+    float t;
+    if (sphere_root(o, d, 0.001f, mk(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z)),
+                    __uint_as_float(v.w & ~kCBvhSphereBit), t))
+      bvh_accept_leaf(h, t, ni, R.cidx);
+    return ni + 1;
+  }
+  const float x0 = (half_lo(v.x) - o.x) * R.ix, x1 = (half_hi(v.y) - o.x) * R.ix;
+  const float y0 = (half_hi(v.x) - o.y) * R.iy, y1 = (half_lo(v.z) - o.y) * R.iy;
+  const float z0 = (half_lo(v.y) - o.z) * R.iz, z1 = (half_hi(v.z) - o.z) * R.iz;
+  const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+  const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+  const float slack = 1e-5f * fabsf(tf) + 1e-7f;
+  const bool hit = tn <= tf + slack && tf >= 0.0f && tn <= h.t * 1.00001f + 1e-7f;
+  const bool leaf = (v.w & kCBvhLeafBit) != 0;
+  if (hit && leaf) {  // a multi-sphere leaf: its spheres in leaf order
+    const int first = (int)((v.w & ~kCBvhLeafBit) >> 3), cnt = (int)(v.w & 7u);
+    for (int j = first; j < first + cnt; j++) {
+      const f4v g0 = geom_g[2 * j], g1 = geom_g[2 * j + 1];  // c, rr | orig
       float t;
-      if (sphere_root(o, d, tmin, mk(a.x, a.y, a.z), b.x, t)) accept(t, __float_as_int(b.y));
-      next = skip;
-    } else {
-      const float x0 = (a.x - o.x) * ix, x1 = (b.x - o.x) * ix;
-      const float y0 = (a.y - o.y) * iy, y1 = (b.y - o.y) * iy;
-      const float z0 = (a.z - o.z) * iz, z1 = (b.z - o.z) * iz;
-      const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
-      const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
-      const float slack = 1e-5f * fabsf(tf) + 1e-7f;
-      const bool hit = tn <= tf + slack && tf >= 0.0f && tn <= h.t * 1.00001f + 1e-7f;
-      if (hit && leaf) {
-        const int first = leaf >> 3, cnt = leaf & 7;
-        for (int j = first; j < first + cnt; j++) {
-          const f4v g0 = geom_g[2 * j], g1 = geom_g[2 * j + 1];  // c, rr | orig
-          float t;
-          if (sphere_root(o, d, tmin, mk(g0.x, g0.y, g0.z), g0.w, t)) accept(t, __float_as_int(g1.x));
-        }
-      }
-      next = (hit && !leaf) ? ni + 1 : skip;
+      if (sphere_root(o, d, 0.001f, mk(g0.x, g0.y, g0.z), g0.w, t)) bvh_accept_orig(h, t, __float_as_int(g1.x), R.cidx);
     }
-    if (next < nn) {
-      a = nodes[2 * next];
-      b = nodes[2 * next + 1];
-    }
+  }
+  return (hit || leaf) ? ni + 1 : (int)v.w;
+}
+// Threaded-BVH walk over the spheres (scenes with >= kBvhMinSpheres).  The
+// brute-force scan in index order with a strict '<' returns the
+// lexicographic minimum of (t, quads before spheres, sphere index); the walk
+// visits spheres in BVH order and keeps that minimum explicitly, so no
+// sphere whose root could win is skipped and the order does not matter.
+RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
+  const BvhRay R = bvh_ray(sc, d);
+  const int nn = sc->n_nodes;
+  GF4* __restrict__ geom_g = (GF4*)sc->sph_geom;  // DevSphereG: 2 x 16 B
+  int ni = 0;
+  u4v v = R.nodes[0];
+  while (ni < nn) {
+    const int next = bvh_visit(geom_g, R, o, d, v, ni, h);
+    if (next < nn) v = R.nodes[next];
     ni = next;
   }
+  bvh_resolve(h, R.cidx);
 }
 
 // The same closest-sphere search over the block's LDS copy of the tree
@@ -414,7 +459,9 @@ RTP_DEV bool quad_hit_axis(const PreExact& E, f3 o, f3 d, float& t_out) {
   return ok1 & !(second & bad2);
 }
 
-template <bool kBvh, bool kLdsBvh = false>
+// kSpheres = false: the quads only (the pool kernel's resumable sphere-BVH
+// walk, spheres_bvh_step, continues from the quads' hit).
+template <bool kBvh, bool kLdsBvh = false, bool kSpheres = true>
 RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefilter,
                         uint32_t* full_out, const float* lds_prex, const LdsBvhNode* lds_bvh = nullptr) {
   Hit h{3.40282347e+38f, -1, 0};
@@ -483,7 +530,8 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
     h.idx = (int)(key & 0xffu);
   }
   static_assert(kQuadKinds == 11, "closest_hit scans every kind");
-  if constexpr (kLdsBvh) {
+  if constexpr (!kSpheres) {
+  } else if constexpr (kLdsBvh) {
     spheres_bvh_lds(lds_bvh, o, d, h);
   } else if constexpr (kBvh) {
     spheres_bvh(sc, o, d, h);
@@ -534,15 +582,15 @@ RTP_DEV unsigned long long stamp(bool on) { return on ? __builtin_amdgcn_s_memti
 // depth-k draws (which + generator, exactly one dead step) to the caller's
 // fast-forward instead of drawing them here.
 // qshade: the block's LDS quad table (fill_qshade).
+template <bool kBvh, bool kDeferDead>
+RTP_DEV int shade_hit(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3& emit, float4* __restrict__ hist_d,
+                      int D, const float* qshade, const Hit h);
 template <bool kBvh, bool kDeferDead = false, bool kLdsBvh = false>
 RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3& emit, float4* __restrict__ hist_d,
                    int D, unsigned long long* dbg, const float* qshade, const LdsBvhNode* lds_bvh = nullptr) {
   const bool st = dbg != nullptr;
   const unsigned long long t0 = stamp(st);
-  const uint32_t t1 = sc->which_t1, t2 = sc->which_t2;
-  const DevLights& L = sc->light;
   const f3 org = ps.org, dir = ps.dir;
-  const int d = ps.d;
   // intersect + CollectIntersecttWorklet (SurfaceWorklets.h:104-109)
   uint32_t fb = 0;  // (stats) 1: this lane ran the exact scan of the prefiltered quads
   Hit h = closest_hit<kBvh, kLdsBvh>(sc, org, dir, true, st ? &fb : nullptr, qshade + kPrexLdsOffset, lds_bvh);
@@ -555,6 +603,19 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
     const unsigned long long t1s = __builtin_amdgcn_s_memtime();
     dbg[kDbgCyclesIntersect] += t1s - t0;
   }
+  return shade_hit<kBvh, kDeferDead>(sc, ps, seed, emit, hist_d, D, qshade, h);
+}
+
+// The rest of one depth once the closest hit h is known: collect, material,
+// generate, pdfs, scatter (bounce() above; the pool kernel's resumable
+// sphere-BVH walk calls it directly for the lanes whose walk has finished).
+template <bool kBvh, bool kDeferDead>
+RTP_DEV int shade_hit(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3& emit, float4* __restrict__ hist_d,
+                      int D, const float* qshade, const Hit h) {
+  const uint32_t t1 = sc->which_t1, t2 = sc->which_t2;
+  const DevLights& L = sc->light;
+  const f3 org = ps.org, dir = ps.dir;
+  const int d = ps.d;
   if (h.kind < 0) {
     if (!kDeferDead) seed = dead_step(seed, t1, t2);  // which + generator draws of the now-dead ray
     return kMissed;
@@ -950,6 +1011,17 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
   bool has_path = false;
   int slot = 0;
   uint32_t seed = 0;
+  // Sphere-BVH scenes (global walk): the closest-hit search is resumable.
+  // A path's walk spans as many loop iterations as it needs; an iteration
+  // walks until RTP_WALK_DONE of the wave's paths have finished theirs, and
+  // only those are shaded.  The walks' lengths differ several-fold between
+  // lanes (C3: 17 of 64 lanes per VALU instruction when every lane's walk ran
+  // to its end inside one iteration); now a long walk no longer holds the
+  // other 63 lanes.  The walk is the same walk (same nodes, same order, same
+  // running minimum), so the hit is bit-identical.
+  constexpr bool kWalk = kBvh && !kLdsBvh;
+  int wni = -1;                             // the path's next BVH node; -1: its quads are not scanned yet
+  Hit wh{3.40282347e+38f, -1, 0};           // its closest hit so far
   Path ps;
   ps.org = eye;
   ps.dir = mk(0.f, 0.f, 1.f);
@@ -1127,10 +1199,46 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
     bool ended = false;
     const unsigned long long ta = stamp(want_dbg);
     unsigned long long tbnc = ta;
-    if (has_path) {
+    bool shade = has_path;
+    if constexpr (kWalk) {
+      const int nn = sc->n_nodes;
+      if (has_path && wni < 0) {  // a new ray: the quads first (their hit bounds the walk)
+        wh = closest_hit<false, false, false>(sc, ps.org, ps.dir, true, nullptr, s_qshade + kPrexLdsOffset);
+        wni = 0;
+      }
+      const uint64_t pm = __ballot(has_path);
+      const int need = min(RTP_WALK_DONE, __popcll(pm));
+      bool walking = has_path && wni < nn;
+      if (__ballot(walking)) {
+        const f3 o = ps.org, d = ps.dir;
+        const BvhRay R = bvh_ray(sc, d);
+        GF4* __restrict__ geom_g = (GF4*)sc->sph_geom;
+        u4v v = u4v{0u, 0u, 0u, 0u};
+        if (walking) v = R.nodes[wni];
+        for (;;) {
+          const uint64_t wm = __ballot(walking);
+          if (wm == 0 || __popcll(pm & ~wm) >= need) break;
+          if (walking) {
+            wni = bvh_visit(geom_g, R, o, d, v, wni, wh);
+            walking = wni < nn;
+            if (walking) v = R.nodes[wni];
+          }
+        }
+        if (has_path && !walking) bvh_resolve(wh, R.cidx);
+      }
+      shade = has_path && !walking;
+      if (want_dbg) dbg[kDbgCyclesIntersect] += stamp(want_dbg) - ta;
+    }
+    if (shade) {
       f3 emit = mk(0.f, 0.f, 0.f);
-      const int res = bounce<kBvh, true, kLdsBvh>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D,
-                                                  want_dbg ? dbg : nullptr, s_qshade, s_bvh);
+      int res;
+      if constexpr (kWalk) {
+        res = shade_hit<kBvh, true>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D, s_qshade, wh);
+        wni = -1;
+      } else {
+        res = bounce<kBvh, true, kLdsBvh>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D,
+                                          want_dbg ? dbg : nullptr, s_qshade, s_bvh);
+      }
       tbnc = stamp(want_dbg);
       if (res == kAlive && ps.d < D - 1) {
         ps.d++;

@@ -106,6 +106,20 @@ struct alignas(16) BvhNode {
 // leaf value of a one-sphere leaf that holds the sphere itself: lo = centre,
 // hi[0] = radius^2, hi[1] = sphere index (int bits)
 constexpr int32_t kBvhLeafSphere = -1;
+// The walks read a compact copy of the octant arrays (DevScene::cnodes, 16 B
+// per node, index for index the BvhNode arrays): one 16-byte gather per node
+// visit instead of two.  On C3 the walk's gathers held the texture data
+// path 91% busy (TD_TD_BUSY, r04d) while VALU issue sat at 0.49.  Four
+// words per node:
+//   sphere leaf (BvhNode::leaf == kBvhLeafSphere): x, y, z = the centre's
+//     float bits, w = r^2 bits | kCBvhSphereBit.  The walk goes on at i + 1
+//     (a leaf's skip); the sphere's scene index is cidx[i], read only for the
+//     final hit and for exact t ties.
+//   inner node or multi-sphere leaf: x = half2(lo.x, lo.y), y = half2(lo.z,
+//     hi.x), z = half2(hi.y, hi.z), each rounded outward (lo down, hi up:
+//     the box only grows, so culling stays conservative); w = skip (inner
+//     node) or kCBvhLeafBit | (first << 3 | count) (leaf: next is i + 1).
+constexpr uint32_t kCBvhSphereBit = 0x80000000u, kCBvhLeafBit = 0x40000000u;
 #ifndef RTP_BVH_EMBED
 #define RTP_BVH_EMBED 1
 #endif
@@ -193,6 +207,8 @@ struct alignas(16) DevScene {
   PreQuad pre[kMaxPre];
   PreExact prex[kMaxPre];  // by quad position (< n_pre)
   const LdsBvhNode* lnodes;  // the LDS walk's tree (global copy, loaded per block; n_lnodes above)
+  const uint32_t* cnodes;    // 8 * n_nodes compact nodes (4 words each; kCBvhSphereBit above)
+  const int32_t* cidx;       // 8 * n_nodes: a sphere leaf's scene index (else -1)
   const void* pad_ptr;
 };
 // The pool kernel's scans prefetch up to two records past the last quad or
