@@ -100,7 +100,7 @@ __global__ void k_boxes(const float4* __restrict__ cr, const uint32_t* __restric
   if (j >= n) return;
   const int leaf = n - 1 + j;
   const float4 s = cr[idx[j]];
-  const float pad = 0.002f * s.w + 1e-5f;
+  const float pad = 0.002f * s.w + 1e-5f + 0x1p-16f * (fmaxf(fabsf(s.x), fmaxf(fabsf(s.y), fabsf(s.z))) + s.w);  // as the host
   blo[leaf] = make_float4(s.x - s.w - pad, s.y - s.w - pad, s.z - s.w - pad, 0.f);
   bhi[leaf] = make_float4(s.x + s.w + pad, s.y + s.w + pad, s.z + s.w + pad, 0.f);
   size[leaf] = 1;

@@ -745,7 +745,10 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     std::vector<BvhPrim> P(s->n_spheres);
     for (int k = 0; k < s->n_spheres; k++) {
       const rtp::DevSphere& S = sph[k];
-      const float pad = 0.002f * S.r + 1e-5f;
+      // (+ 2^-16 of the coordinates' magnitude: the walk's fma slab test,
+      // rtp_kernels.hip BvhRay, stays far inside the margin at any scale)
+      const float pad = 0.002f * S.r + 1e-5f +
+                        0x1p-16f * (std::max(std::fabs(S.c[0]), std::max(std::fabs(S.c[1]), std::fabs(S.c[2]))) + S.r);
       for (int a = 0; a < 3; a++) {
         P[k].lo[a] = S.c[a] - S.r - pad;
         P[k].hi[a] = S.c[a] + S.r + pad;

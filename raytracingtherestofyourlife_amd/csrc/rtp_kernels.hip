@@ -49,6 +49,12 @@ constexpr int kHistChunk = 4;
 // many of the wave's paths have finished their walks (or all have)
 #define RTP_WALK_DONE 48
 #endif
+#ifndef RTP_WALK_FMA
+#define RTP_WALK_FMA 1  // the walk's slab test as fma(box, 1/d, -o/d) (BvhRay)
+#endif
+#ifndef RTP_WALK_PREFETCH
+#define RTP_WALK_PREFETCH 0  // the pool walk loads node i + 1 while testing node i
+#endif
 #ifndef RTP_CRIT_FF
 #define RTP_CRIT_FF 100  // pool kernel: lag (per mille of the wave's average samples) that makes a pixel critical
 #endif
@@ -151,15 +157,31 @@ RTP_DEV float slab_rcp(float v) { return __builtin_amdgcn_rcpf(fabsf(v) < 1e-20f
 // near-to-far for its direction octant (rtp_layout.hpp kCBvhSphereBit) and
 // that copy's sphere-index table.  (Global, address space 1, pointers: through
 // the generic ones loaded from the scene the walk compiled to flat loads.)
+// The slab test runs as fma(box, 1/d, -o/d): one rounding of o/d per
+// component instead of a rounded (box - o) per face.  The boxes only cull,
+// and each sphere lies at least the host's pad inside its boxes on every
+// axis (rtp_host.cpp: 0.002 r + 1e-5 + 2^-16 (|c| + r)), so a ray through
+// a sphere crosses every box around it over a parameter interval 2 pad / |d|
+// wider than the sphere's: far above these roundings (2^-24 |o| / |d|).
 struct BvhRay {
   GU4* nodes;
   GI32* cidx;
-  float ix, iy, iz;
+  float ix, iy, iz;     // 1/d (clamped)
+  float ox, oy, oz;     // -o/d
 };
-RTP_DEV BvhRay bvh_ray(const DevScene* __restrict__ sc, f3 d) {
+RTP_DEV BvhRay bvh_ray(const DevScene* __restrict__ sc, f3 o, f3 d) {
   const int oct = (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0);
   const int64_t base = (int64_t)oct * sc->n_nodes;
-  return BvhRay{(GU4*)(sc->cnodes + 4 * base), (GI32*)(sc->cidx + base), slab_rcp(d.x), slab_rcp(d.y), slab_rcp(d.z)};
+  BvhRay R;
+  R.nodes = (GU4*)(sc->cnodes + 4 * base);
+  R.cidx = (GI32*)(sc->cidx + base);
+  R.ix = slab_rcp(d.x);
+  R.iy = slab_rcp(d.y);
+  R.iz = slab_rcp(d.z);
+  R.ox = -(o.x * R.ix);
+  R.oy = -(o.y * R.iy);
+  R.oz = -(o.z * R.iz);
+  return R;
 }
 // During a walk a sphere hit is h.kind == 2 with h.idx the leaf's node (the
 // sphere's scene index is cidx[node]); bvh_resolve turns it into kind 1 with
@@ -206,9 +228,15 @@ RTP_DEV int bvh_visit(GF4* __restrict__ geom_g, const BvhRay& R, f3 o, f3 d, u4v
       bvh_accept_leaf(h, t, ni, R.cidx);
     return ni + 1;
   }
+#if RTP_WALK_FMA
+  const float x0 = __builtin_fmaf(half_lo(v.x), R.ix, R.ox), x1 = __builtin_fmaf(half_hi(v.y), R.ix, R.ox);
+  const float y0 = __builtin_fmaf(half_hi(v.x), R.iy, R.oy), y1 = __builtin_fmaf(half_lo(v.z), R.iy, R.oy);
+  const float z0 = __builtin_fmaf(half_lo(v.y), R.iz, R.oz), z1 = __builtin_fmaf(half_hi(v.z), R.iz, R.oz);
+#else
   const float x0 = (half_lo(v.x) - o.x) * R.ix, x1 = (half_hi(v.y) - o.x) * R.ix;
   const float y0 = (half_hi(v.x) - o.y) * R.iy, y1 = (half_lo(v.z) - o.y) * R.iy;
   const float z0 = (half_lo(v.y) - o.z) * R.iz, z1 = (half_hi(v.z) - o.z) * R.iz;
+#endif
   const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
   const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
   const float slack = 1e-5f * fabsf(tf) + 1e-7f;
@@ -219,7 +247,8 @@ RTP_DEV int bvh_visit(GF4* __restrict__ geom_g, const BvhRay& R, f3 o, f3 d, u4v
     for (int j = first; j < first + cnt; j++) {
       const f4v g0 = geom_g[2 * j], g1 = geom_g[2 * j + 1];  // c, rr | orig
       float t;
-      if (sphere_root(o, d, 0.001f, mk(g0.x, g0.y, g0.z), g0.w, t)) bvh_accept_orig(h, t, __float_as_int(g1.x), R.cidx);
+      if (sphere_root(o, d, 0.001f, mk(g0.x, g0.y, g0.z), g0.w, t))
+        bvh_accept_orig(h, t, __float_as_int(g1.x), R.cidx);
     }
   }
   return (hit || leaf) ? ni + 1 : (int)v.w;
@@ -230,7 +259,7 @@ RTP_DEV int bvh_visit(GF4* __restrict__ geom_g, const BvhRay& R, f3 o, f3 d, u4v
 // visits spheres in BVH order and keeps that minimum explicitly, so no
 // sphere whose root could win is skipped and the order does not matter.
 RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
-  const BvhRay R = bvh_ray(sc, d);
+  const BvhRay R = bvh_ray(sc, o, d);
   const int nn = sc->n_nodes;
   GF4* __restrict__ geom_g = (GF4*)sc->sph_geom;  // DevSphereG: 2 x 16 B
   int ni = 0;
@@ -1211,17 +1240,31 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
       bool walking = has_path && wni < nn;
       if (__ballot(walking)) {
         const f3 o = ps.org, d = ps.dir;
-        const BvhRay R = bvh_ray(sc, d);
+        const BvhRay R = bvh_ray(sc, o, d);
         GF4* __restrict__ geom_g = (GF4*)sc->sph_geom;
         u4v v = u4v{0u, 0u, 0u, 0u};
         if (walking) v = R.nodes[wni];
+#if RTP_WALK_PREFETCH
+        // node i + 1 is loaded while node i is tested: the walk goes on there
+        // after a hit inner node or a sphere leaf (only a missed box skips)
+        u4v vn = u4v{0u, 0u, 0u, 0u};
+        if (walking && wni + 1 < nn) vn = R.nodes[wni + 1];
+#endif
         for (;;) {
           const uint64_t wm = __ballot(walking);
           if (wm == 0 || __popcll(pm & ~wm) >= need) break;
           if (walking) {
-            wni = bvh_visit(geom_g, R, o, d, v, wni, wh);
-            walking = wni < nn;
-            if (walking) v = R.nodes[wni];
+            const int next = bvh_visit(geom_g, R, o, d, v, wni, wh);
+            walking = next < nn;
+#if RTP_WALK_PREFETCH
+            if (walking) {
+              v = next == wni + 1 ? vn : R.nodes[next];
+              if (next + 1 < nn) vn = R.nodes[next + 1];
+            }
+#else
+            if (walking) v = R.nodes[next];
+#endif
+            wni = next;
           }
         }
         if (has_path && !walking) bvh_resolve(wh, R.cidx);

@@ -109,7 +109,7 @@ constexpr int32_t kBvhLeafSphere = -1;
 // The walks read a compact copy of the octant arrays (DevScene::cnodes, 16 B
 // per node, index for index the BvhNode arrays): one 16-byte gather per node
 // visit instead of two.  On C3 the walk's gathers held the texture data
-// path 91% busy (TD_TD_BUSY, r04d) while VALU issue sat at 0.49.  Four
+// path 91% busy (TD_TD_BUSY, r03t) while VALU issue sat at 0.49.  Four
 // words per node:
 //   sphere leaf (BvhNode::leaf == kBvhLeafSphere): x, y, z = the centre's
 //     float bits, w = r^2 bits | kCBvhSphereBit.  The walk goes on at i + 1

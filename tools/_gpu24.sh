@@ -1,0 +1,5 @@
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r04f
+bash tools/gpu_step.sh \
+ "200 r04f_pmc_ta.log rocprofv3 --pmc TA_TA_BUSY_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU --kernel-trace -d gpurun_out/r04f/pmc_ta -o run --output-format csv -- python3 tools/quick_bench.py --nx 2048 --ny 2048 --spp 16 --variant 3 --reps 1" \
+ "900 r04f_ab_c3.log bash tools/ab_c3.sh 2 main variants/d40.so variants/d56.so"
