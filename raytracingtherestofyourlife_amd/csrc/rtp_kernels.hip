@@ -49,12 +49,6 @@ constexpr int kHistChunk = 4;
 // many of the wave's paths have finished their walks (or all have)
 #define RTP_WALK_DONE 48
 #endif
-#ifndef RTP_WALK_FMA
-#define RTP_WALK_FMA 1  // the walk's slab test as fma(box, 1/d, -o/d) (BvhRay)
-#endif
-#ifndef RTP_WALK_PREFETCH
-#define RTP_WALK_PREFETCH 0  // the pool walk loads node i + 1 while testing node i
-#endif
 #ifndef RTP_CRIT_FF
 #define RTP_CRIT_FF 100  // pool kernel: lag (per mille of the wave's average samples) that makes a pixel critical
 #endif
@@ -228,15 +222,9 @@ RTP_DEV int bvh_visit(GF4* __restrict__ geom_g, const BvhRay& R, f3 o, f3 d, u4v
       bvh_accept_leaf(h, t, ni, R.cidx);
     return ni + 1;
   }
-#if RTP_WALK_FMA
   const float x0 = __builtin_fmaf(half_lo(v.x), R.ix, R.ox), x1 = __builtin_fmaf(half_hi(v.y), R.ix, R.ox);
   const float y0 = __builtin_fmaf(half_hi(v.x), R.iy, R.oy), y1 = __builtin_fmaf(half_lo(v.z), R.iy, R.oy);
   const float z0 = __builtin_fmaf(half_lo(v.y), R.iz, R.oz), z1 = __builtin_fmaf(half_hi(v.z), R.iz, R.oz);
-#else
-  const float x0 = (half_lo(v.x) - o.x) * R.ix, x1 = (half_hi(v.y) - o.x) * R.ix;
-  const float y0 = (half_hi(v.x) - o.y) * R.iy, y1 = (half_lo(v.z) - o.y) * R.iy;
-  const float z0 = (half_lo(v.y) - o.z) * R.iz, z1 = (half_hi(v.z) - o.z) * R.iz;
-#endif
   const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
   const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
   const float slack = 1e-5f * fabsf(tf) + 1e-7f;
@@ -1244,26 +1232,13 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
         GF4* __restrict__ geom_g = (GF4*)sc->sph_geom;
         u4v v = u4v{0u, 0u, 0u, 0u};
         if (walking) v = R.nodes[wni];
-#if RTP_WALK_PREFETCH
-        // node i + 1 is loaded while node i is tested: the walk goes on there
-        // after a hit inner node or a sphere leaf (only a missed box skips)
-        u4v vn = u4v{0u, 0u, 0u, 0u};
-        if (walking && wni + 1 < nn) vn = R.nodes[wni + 1];
-#endif
         for (;;) {
           const uint64_t wm = __ballot(walking);
           if (wm == 0 || __popcll(pm & ~wm) >= need) break;
           if (walking) {
             const int next = bvh_visit(geom_g, R, o, d, v, wni, wh);
             walking = next < nn;
-#if RTP_WALK_PREFETCH
-            if (walking) {
-              v = next == wni + 1 ? vn : R.nodes[next];
-              if (next + 1 < nn) vn = R.nodes[next + 1];
-            }
-#else
             if (walking) v = R.nodes[next];
-#endif
             wni = next;
           }
         }
