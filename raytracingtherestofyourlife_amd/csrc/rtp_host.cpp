@@ -23,6 +23,7 @@
 #include "rtp_layout.hpp"
 
 extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int bvh, int* variant_out, int* waves_out);
+extern "C" int rtp_plan_steal(int64_t npix, int bvh);
 extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::KParams* p, int variant, int waves, int bvh,
                                         hipStream_t stream, int n_lnodes);
 extern "C" hipError_t rtp_launch_eval_primitive(int kind, const void* in, void* out, int64_t n, const uint32_t* tab,
@@ -577,7 +578,7 @@ rtp_status rtp_create(int32_t device, rtp_context** out) {
     delete c;
     return hip_fail(e, "hipMalloc(scene)");
   }
-  e = hipMalloc(&c->d_progress, 8);
+  e = hipMalloc(&c->d_progress, 16);
   if (e != hipSuccess) {
     (void)hipFree(c->d_scene);
     delete c;
@@ -973,6 +974,16 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
     lanes = (int64_t)plan_waves * 128;
   }
   p.wave_begin = d_wave_begin;
+  // more entries than the resident waves' pools hold: the resident waves
+  // steal entries (RTP_STEAL=0: waves of 128 entries in generations)
+  if (variant == 2 && !d_wave_begin && !stats_on && spp > 0) {
+    const char* se = getenv("RTP_STEAL");
+    const int sw = (se && se[0] == '0') ? 0 : rtp_plan_steal(npix, bvh);
+    if (sw > 0) {
+      waves = sw;
+      lanes = (int64_t)sw * 128;
+    }
+  }
   // D rows per lane (row k of a light hit holds E_k), rounded up to 8 (a
   // slot-major history pads each slot to whole 128-byte lines)
   size_t hist_need = (size_t)((depth + 7) & ~7) * (size_t)lanes * 16;
@@ -987,7 +998,7 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
     p.ffd = ft.direct, p.ffd_first = ft.d_first, p.ffd_count = ft.d_count;
   }
   if (c->pending) HIP_TRY(hipStreamWaitEvent(stream, c->done, 0));
-  HIP_TRY(hipMemsetAsync(c->d_progress, 0, 8, stream));
+  HIP_TRY(hipMemsetAsync(c->d_progress, 0, 16, stream));  // [0] progress, [1] entries stolen (kSteal)
   {
     const char* e = getenv("RTP_DEBUG_STATS");
     if (e && (e[0] == '1' || e[0] == '2') && variant == 2) {  // 2: timestamps in the production kernel

@@ -944,9 +944,15 @@ typedef const __attribute__((address_space(1))) uint32_t GU32;
 // expected cost -- instead of the interleaved entries j * n_waves + w.
 // The pool kernel's body; kWPB waves per block, kLdsBvh: the sphere BVH is
 // walked out of the block's LDS copy (s_bvh, rtp_render_pool_lds).
-template <bool kStats, bool kBvh, bool kTiles, bool kPlan, int kWPB, bool kLdsBvh>
+// kSteal: a launch with more entries than its waves' pools hold (C3, C4,
+// C5 on one GPU).  The waves are the resident ones; a slot whose pixel has
+// all its samples writes the pixel out and claims the next unclaimed entry
+// (one atomic per batch), so no wave idles while entries remain, instead of
+// waves of 128 pixels each running in generations with a tail per wave.
+template <bool kStats, bool kBvh, bool kTiles, bool kPlan, int kWPB, bool kLdsBvh, bool kSteal = false>
 __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const KParams& p, int n_waves,
-                                          unsigned char* smem, float* s_qshade, LdsBvhNode* s_bvh) {
+                                          unsigned char* smem, float* s_qshade, LdsBvhNode* s_bvh,
+                                          uint32_t* s_entry_all = nullptr) {
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
   const int w = blockIdx.x * kWPB + wib;  // global wave id
@@ -970,6 +976,7 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
   uint16_t* s_rem = reinterpret_cast<uint16_t*>(s_live + kPool);
   uint16_t* q_ready = s_rem + kPool;
   uint16_t* q_ff = q_ready + kPool;
+  uint32_t* s_entry = kSteal ? s_entry_all + wib * kPool : nullptr;  // kSteal: the slot's entry
 
   const uint32_t t1 = sc->which_t1, t2 = sc->which_t2;
   const int D = p.depth, S = p.spp;
@@ -985,6 +992,7 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
   }
   for (int j = lane; j < n_slots; j += 64) {
     const int64_t k = kPlan ? (int64_t)(wbase + j) : (int64_t)j * n_waves + w;
+    if constexpr (kSteal) s_entry[j] = (uint32_t)k;
     s_seed[j] = p.seed_base + (uint32_t)pixel_of<kTiles>(p, k);  // seeds[i] = i (MapperPathTracer.cxx:265-267)
     s_r[j] = 0.f;
     s_g[j] = 0.f;
@@ -1023,6 +1031,9 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
   }
 
   int published = 0;  // wave-uniform: finished samples already added to p.progress
+  // kSteal (wave-uniform): slots still holding a pixel, and the samples of the
+  // pixels already written out (the fair-share average is over the others)
+  int live_slots = n_slots, retired = 0;
   bool critical_ff = false;  // wave-uniform: a critical (far-lagging) pixel waits in the FF queue
 
   bool has_path = false;
@@ -1161,6 +1172,38 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
       if (mine) s_seed[fslot] = fseed;
       if (mine) again = s_samples[fslot] < (uint32_t)S;
       if (want_dbg) unfinished -= __popcll(__ballot(mine && !again));
+      if constexpr (kSteal) {
+        // pixels with all their samples: written out, their slots take the
+        // next unclaimed entries (claimed in launch order after the initial
+        // n_waves * kPool)
+        const uint64_t done = __ballot(mine && !again);
+        if (done) {
+          const int nd = __popcll(done);
+          unsigned long long base = 0;
+          if (lane == 0) base = atomicAdd(kparams().progress + 1, (unsigned long long)nd);
+          base = __shfl(base, 0) + (unsigned long long)n_waves * kPool;
+          retired += nd * S;
+          if (mine && !again) {
+            const int64_t k = (int64_t)s_entry[fslot];
+            reinterpret_cast<float4*>(p.out)[k] = make_float4(s_r[fslot], s_g[fslot], s_b[fslot], 0.f);
+            if (p.seed_out) p.seed_out[k] = s_seed[fslot];
+            if (p.live_out) p.live_out[k] = s_live[fslot];
+            const unsigned long long kn = base + lane_rank(done);
+            if (kn < (unsigned long long)p.npix) {  // a fresh pixel in this slot, at the front of READY below
+              s_entry[fslot] = (uint32_t)kn;
+              s_seed[fslot] = p.seed_base + (uint32_t)pixel_of<kTiles>(p, (int)kn);
+              s_r[fslot] = 0.f;
+              s_g[fslot] = 0.f;
+              s_b[fslot] = 0.f;
+              s_samples[fslot] = 0u;
+              s_live[fslot] = 0u;
+              s_rem[fslot] = 0;
+              again = true;
+            }
+          }
+          live_slots -= __popcll(__ballot(mine && !again));
+        }
+      }
       // Fair share: a pixel whose completed samples are at or below the
       // wave's average (ff_tail / n_slots) goes to the FRONT of the READY
       // ring, the others to the back.  FIFO alone let cheap pixels (short
@@ -1168,7 +1211,8 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
       // expensive pixels' sequential sample chains ran on alone at the end
       // (17% of bounce steps with ~12 of 64 lanes live).
       // (samples * n_slots <= 2^23 * 2^8 and ff_tail <= n_slots * spp: 32 bits suffice)
-      const bool urgent = again && s_samples[fslot] * (uint32_t)n_slots <= (uint32_t)ff_tail;
+      const bool urgent = again && (kSteal ? s_samples[fslot] * (uint32_t)live_slots <= (uint32_t)(ff_tail - retired)
+                                           : s_samples[fslot] * (uint32_t)n_slots <= (uint32_t)ff_tail);
       const uint64_t pu = __ballot(urgent), pn = __ballot(again && !urgent);
       ready_head -= __popcll(pu);
       if (urgent) q_ready[(ready_head + (int)lane_rank(pu)) & (kPool - 1)] = (uint16_t)fslot;
@@ -1201,7 +1245,8 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
         // segment pointer: &p would copy p to scratch)
         CKP& P = kparams();
         int pi, pj;
-        pixel_xy<kTiles>(P, kPlan ? wbase + slot : slot * n_waves + w, pi, pj);  // (32-bit index: a 64-bit one spilled)
+        pixel_xy<kTiles>(P, kSteal ? (int)s_entry[slot] : kPlan ? wbase + slot : slot * n_waves + w, pi,
+                         pj);  // (32-bit index: a 64-bit one spilled)
         ps.dir = camera_ray(P.cam, pi, pj, P.nx, P.ny, seed);
         ps.org = ld3(P.cam.eye);
         ps.d = 0;
@@ -1287,8 +1332,9 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
     // RTP_CRIT_FF/1000 runs its sample chain on the critical path (its path
     // length keeps it behind): its fast-forward is not left waiting for the
     // READY queue to run dry -- the batch runs in the next iteration.
-    // (a scheduling heuristic: single precision is plenty)
-    if (__ballot(ended && (float)(s_samples[slot] * (uint32_t)n_slots) * 1000.0f <
+    // (a scheduling heuristic: single precision is plenty; kSteal: fresh
+    // pixels always lag, so no critical batches)
+    if (!kSteal && __ballot(ended && (float)(s_samples[slot] * (uint32_t)n_slots) * 1000.0f <
                               (float)ff_tail * (float)(1000 - RTP_CRIT_FF)))
       critical_ff = true;
 #endif
@@ -1325,7 +1371,7 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
       if (c != kDbgRealStart && c != kDbgHwId) p.dbg[(int64_t)w * kDbgCounters + c] = dbg[c];
   }
   wave_sync();
-  for (int j = lane; j < n_slots; j += 64) {
+  for (int j = lane; j < (kSteal ? 0 : n_slots); j += 64) {  // (kSteal: written as they finished)
     const int64_t k = kPlan ? (int64_t)(wbase + j) : (int64_t)j * n_waves + w;
     reinterpret_cast<float4*>(p.out)[k] = make_float4(s_r[j], s_g[j], s_b[j], 0.f);
     if (p.seed_out) p.seed_out[k] = s_seed[j];
@@ -1338,12 +1384,18 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
 #else
 #define RTP_POOL_VGPR_ATTR
 #endif
-template <bool kStats, bool kBvh, bool kTiles = false, bool kPlan = false>
+template <bool kStats, bool kBvh, bool kTiles = false, bool kPlan = false, bool kSteal = false>
 __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_ATTR
     rtp_render_pool(const DevScene* __restrict__ sc, KParams p, int n_waves) {
   __shared__ __align__(16) unsigned char smem[kPoolLdsBytes];
   __shared__ __align__(16) float s_qshade[kQTableFloats];
-  pool_body<kStats, kBvh, kTiles, kPlan, kWavesPerBlock, false>(sc, p, n_waves, smem, s_qshade, nullptr);
+  if constexpr (kSteal) {
+    __shared__ uint32_t s_entry[kWavesPerBlock * kPool];
+    pool_body<kStats, kBvh, kTiles, kPlan, kWavesPerBlock, false, true>(sc, p, n_waves, smem, s_qshade, nullptr,
+                                                                        s_entry);
+  } else {
+    pool_body<kStats, kBvh, kTiles, kPlan, kWavesPerBlock, false>(sc, p, n_waves, smem, s_qshade, nullptr);
+  }
 }
 
 // Scenes whose sphere BVH fits the LDS (LdsBvhNode, <= kLdsBvhMaxNodes):
@@ -1553,6 +1605,15 @@ extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int bvh, int* variant_ou
   return W * rtp::kPool;
 }
 
+// Work stealing (pool_body kSteal) when a launch's entries exceed what the
+// resident waves' pools hold: the resident waves, each refilling its slots
+// from the unclaimed entries.  Returns the waves (0: no stealing).
+extern "C" int rtp_plan_steal(int64_t npix, int bvh) {
+  if (bvh == 2) return 0;  // (the LDS walk's kernel has no stealing instance)
+  const int64_t resident = pool_resident_waves(false, bvh);
+  return npix > resident * rtp::kPool ? (int)resident : 0;
+}
+
 extern "C" hipError_t rtp_launch_eval_closest(const rtp::DevScene* scene, const float* rays, uint32_t* out,
                                               int64_t n, int bvh, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
@@ -1588,6 +1649,15 @@ extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::K
       if (bvh || p->tile_world > 0) return hipErrorNotSupported;
       if (stats) hipLaunchKernelGGL((rtp::rtp_render_pool<true, false, false, true>), g, b, 0, stream, scene, *p, waves);
       else hipLaunchKernelGGL((rtp::rtp_render_pool<false, false, false, true>), g, b, 0, stream, scene, *p, waves);
+    } else if ((int64_t)waves * rtp::kPool < p->npix) {  // more entries than slots: work stealing (rtp_plan_steal)
+      if (stats) return hipErrorNotSupported;
+      if (p->tile_world > 0) {
+        if (bvh) hipLaunchKernelGGL((rtp::rtp_render_pool<false, true, true, false, true>), g, b, 0, stream, scene, *p, waves);
+        else hipLaunchKernelGGL((rtp::rtp_render_pool<false, false, true, false, true>), g, b, 0, stream, scene, *p, waves);
+      } else {
+        if (bvh) hipLaunchKernelGGL((rtp::rtp_render_pool<false, true, false, false, true>), g, b, 0, stream, scene, *p, waves);
+        else hipLaunchKernelGGL((rtp::rtp_render_pool<false, false, false, false, true>), g, b, 0, stream, scene, *p, waves);
+      }
     } else if (p->tile_world > 0) {  // the tile deal: its own instances, no stats variant
       if (bvh) hipLaunchKernelGGL((rtp::rtp_render_pool<false, true, true>), g, b, 0, stream, scene, *p, waves);
       else hipLaunchKernelGGL((rtp::rtp_render_pool<false, false, true>), g, b, 0, stream, scene, *p, waves);

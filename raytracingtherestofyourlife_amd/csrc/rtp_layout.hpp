@@ -249,7 +249,8 @@ struct KParams {
   uint32_t* live_out;        // nullable
   float* hist;               // float4[(depth-1) * lanes] attenuation history, depth-major
   unsigned long long* dbg;   // nullable: per-wave counters (kDbgCounters each), diagnostics only
-  unsigned long long* progress;  // zeroed before launch: samples finished by all waves (issue-priority balancing)
+  unsigned long long* progress;  // 2 words zeroed before launch: [0] samples finished by all waves (issue-priority
+                                 // balancing), [1] entries claimed by work stealing (pool kernel kSteal)
   // RNG jump tables (nullable): ff[j][s] = the state after (32 >> j) dead
   // depths from state s (2^32 entries each, 16 GiB; rtp_host.cpp)
   const uint32_t* ff[kFfTables];

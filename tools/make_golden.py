@@ -148,6 +148,14 @@ def main():
                    seed_base=(3 * 3840 * 2160) % (1 << 32))
     # C3 (BASELINE configs[2]): 1000-sphere scene, 2048x2048, 256 spp, depth 50 (assumed)
     render_fixture("c3_subset", 3, 2048, 2048, 256, 50, pixels=subset(2048 * 2048, 1024, 12))
+    # round 3: wider config-scale checks (VERDICT r02 "what's weak" #1)
+    # C4 at full S x D on 16384 pixels (64x c4_subset)
+    render_fixture("c4_subset16k", 0, 1920, 1080, 4096, 50, pixels=subset(1920 * 1080, 16384, 14))
+    # one C5 sample-batch shard at its real length: S = 16384 over 8 GPUs = 2048 spp, shard 3
+    render_fixture("c5_shard3_2048spp", 0, 3840, 2160, 2048, 50, pixels=subset(3840 * 2160, 1024, 15),
+                   seed_base=(3 * 3840 * 2160) % (1 << 32))
+    # C3 at full S x D on 4096 pixels (4x c3_subset)
+    render_fixture("c3_subset4k", 3, 2048, 2048, 256, 50, pixels=subset(2048 * 2048, 4096, 16))
     # -direct mode (main.cc:120-251, 623-651): the default camera at the
     # reference's default canvas (128x128), a non-square canvas, a hemisphere
     # view (generate(): phi 0.4, theta 1.2566371) and a camera inside the box
