@@ -457,12 +457,39 @@ int bvh_build(std::vector<BvhPrim>& P, int b, int e, std::vector<TNode>& T, std:
   return me;
 }
 
+// inner nodes of the sphere BVH above this depth are dropped from the walks'
+// arrays (bvh_flatten below)
+constexpr int kBvhDropDepth = 0;
+constexpr float kBvhDropArea = 0.f;  // (0: off)
+
 // threaded flattening for one octant (bit k set: direction component k < 0)
 // A one-sphere leaf carries the sphere itself (rtp::kBvhLeafSphere): lo =
 // centre, hi[0] = r*r, hi[1] = the sphere's index (as int bits), so the walk
 // runs the exact root test without a box test or a second dependent load.
+// Inner nodes above depth `drop` are not emitted: their children take their
+// place in the order (the skip of the node before them then lands on their
+// first emitted descendant), so the walk treats their boxes as hit.  A box
+// only culls, so this changes which nodes a ray visits, never its hit.  The
+// top boxes (the whole sphere cloud, its halves) are hit by nearly every ray
+// from inside the room: each one dropped is one dependent gather and box test
+// fewer per walk.
+// Below that, with drop_sa > 0, an inner node with two inner children is
+// dropped too when its surface area exceeds drop_sa of its parent's (a ray
+// that reaches it would hit its box with about that probability: dropping it
+// saves one visit when it would be hit and costs one when it would not).
 void bvh_flatten(const std::vector<TNode>& T, int t, int oct, const std::vector<int32_t>& order,
-                 const std::vector<rtp::DevSphere>& sph, std::vector<rtp::BvhNode>& out) {
+                 const std::vector<rtp::DevSphere>& sph, std::vector<rtp::BvhNode>& out, int depth = 0,
+                 int drop = 0, float drop_sa = 0.f, float parent_area = 0.f) {
+  const TNode& n = T[t];
+  const float area = half_area(n.lo, n.hi);
+  const bool inner2 = n.left >= 0 && T[n.left].left >= 0 && T[n.right].left >= 0;
+  if (n.left >= 0 && (depth < drop || (drop_sa > 0.f && inner2 && parent_area > 0.f && area > drop_sa * parent_area))) {
+    const bool neg = (oct >> n.axis) & 1;
+    const float pa = parent_area > 0.f ? parent_area : area;  // the nearest emitted ancestor's (or the root's)
+    bvh_flatten(T, neg ? n.right : n.left, oct, order, sph, out, depth + 1, drop, drop_sa, pa);
+    bvh_flatten(T, neg ? n.left : n.right, oct, order, sph, out, depth + 1, drop, drop_sa, pa);
+    return;
+  }
   const int me = (int)out.size();
   out.emplace_back();
   rtp::BvhNode nd{};
@@ -483,8 +510,8 @@ void bvh_flatten(const std::vector<TNode>& T, int t, int oct, const std::vector<
     }
   } else {
     const bool neg = (oct >> s.axis) & 1;  // moving toward lower coordinates: right (upper) child first
-    bvh_flatten(T, neg ? s.right : s.left, oct, order, sph, out);
-    bvh_flatten(T, neg ? s.left : s.right, oct, order, sph, out);
+    bvh_flatten(T, neg ? s.right : s.left, oct, order, sph, out, depth + 1, drop, drop_sa, area);
+    bvh_flatten(T, neg ? s.left : s.right, oct, order, sph, out, depth + 1, drop, drop_sa, area);
     nd.leaf = 0;
   }
   nd.skip = (int32_t)out.size();
@@ -766,9 +793,16 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     // diverge as much as on the global walk (13 vs 17 of 64 per instruction)
     const char* le = getenv("RTP_BVH_LDS");
     if (le && le[0] == '1' && bvh_lds_layout(tree, order, sph, lnodes)) h->n_lnodes = (int32_t)lnodes.size();
+    // inner nodes above this depth are not emitted (bvh_flatten; RTP_BVH_DROP overrides)
+    int drop = kBvhDropDepth;
+    float drop_sa = kBvhDropArea;
+    if (const char* dd = getenv("RTP_BVH_DROP")) drop = std::max(0, std::min(16, atoi(dd)));
+    if (const char* da = getenv("RTP_BVH_DROP_SA")) drop_sa = (float)atof(da);
+    int per_oct = 0;
     for (int oct = 0; oct < 8; oct++) {  // 8 copies of n_nodes entries, indices local to each copy
       std::vector<rtp::BvhNode> one;
-      bvh_flatten(tree, 0, oct, order, sph, one);
+      bvh_flatten(tree, 0, oct, order, sph, one, 0, drop, drop_sa);
+      per_oct = (int)one.size();  // (the same nodes are dropped in every octant's order)
       nodes.insert(nodes.end(), one.begin(), one.end());
     }
     geom.resize(order.size());
@@ -779,7 +813,7 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
       geom[j].rr = S.rr;
       geom[j].orig = order[j];
     }
-    h->n_nodes = (int32_t)tree.size();
+    h->n_nodes = (int32_t)per_oct;
   }
   h->n_spheres = s->n_spheres;
   // lights (MapperPathTracer.cxx:141-148): light quad = light_box_pointids[1..4]

@@ -156,3 +156,22 @@ def test_lds_walk_equals_global_walk_c3(rtp, device, monkeypatch):
     assert_render_equal(out["lds"], out["global"], "C3: LDS walk vs global walk")
     assert_render_equal(out["lds_tiles"], out["lds"], "C3: LDS walk, tile-deal instance vs pixel list")
     assert_render_equal(out["global_tiles"], out["global"], "C3: global walk, tile-deal instance vs pixel list")
+
+
+@pytest.mark.parametrize("drop", [0, 1, 3, 8])
+def test_dropped_top_nodes_match_oracle(rtp, oracle, device, monkeypatch, drop):
+    """Inner nodes above depth `drop` left out of the walks' arrays
+    (rtp_host.cpp bvh_flatten, RTP_BVH_DROP): their boxes count as hit, so the
+    walk visits more nodes but finds the same (t, index) minimum -- bit-exact
+    against the oracle's brute-force closest hit (1200 spheres; 8 drops most
+    of the tree's inner levels)."""
+    sc = _oracle_scene(oracle, 1200, 33)
+    nx = ny = 128
+    pix = np.sort(np.random.default_rng(9).choice(nx * ny, 384, replace=False)).astype(np.int64)
+    want = oracle.render_pixels(sc, oracle.camera_setup(nx, ny), nx, ny, 4, 50, pix)
+    monkeypatch.setenv("RTP_BVH_BUILD", "host")
+    monkeypatch.setenv("RTP_BVH_DROP", str(drop))
+    set_scene_from_oracle(device, sc)
+    assert_render_equal(_render(device, rtp, nx, ny, 4, 50, pix), want, f"sphere BVH without its top {drop} levels")
+    monkeypatch.delenv("RTP_BVH_DROP")
+    device.set_cornell_box(0)
