@@ -459,8 +459,8 @@ int bvh_build(std::vector<BvhPrim>& P, int b, int e, std::vector<TNode>& T, std:
 
 // inner nodes of the sphere BVH above this depth are dropped from the walks'
 // arrays (bvh_flatten below)
-constexpr int kBvhDropDepth = 0;
-constexpr float kBvhDropArea = 0.f;  // (0: off)
+constexpr int kBvhDropDepth = 2;
+constexpr float kBvhDropArea = 0.6f;  // (0: off)
 
 // threaded flattening for one octant (bit k set: direction component k < 0)
 // A one-sphere leaf carries the sphere itself (rtp::kBvhLeafSphere): lo =
