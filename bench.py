@@ -1,16 +1,22 @@
 """Benchmark of the path-tracing hot path (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload auto|c2|c4] [--scaling strong|weak]
 
-One step = one full render of the C2 workload: Cornell Box 800x800, 1000 spp,
-depth 50 (BASELINE.json configs[1]), the metric's own image.
+One step = one full render of the workload's frame.
+  c2: Cornell Box 800x800, 1000 spp, depth 50 (BASELINE.json configs[1]), the
+      metric's own image: the N = 1 workload (--workload auto).
+  c4: Cornell Box 1920x1080, 4096 spp, depth 50 (BASELINE.json configs[3]),
+      the configuration BASELINE.json names for the 2/4/8-GPU image-tile
+      shard: the N > 1 workload (--workload auto).  On one GPU it renders at
+      the same rate as C2 (5591 vs 5646 Msamples/s, r03z2), so the driver's
+      N-GPU / 1-GPU ratio compares like with like.
 N > 1 (launched by torch.distributed.run, one process per GPU):
-  --scaling strong (default): THE 800x800 frame, its 16x16 tiles dealt to the
-      ranks round-robin; each rank renders 1/N of the
-      pixels, and the float4 framebuffer is summed to rank 0 with ONE reduce
-      per step (RCCL over xGMI), overlapped with the next step's render (two
-      canvases, alternating; exact: every pixel is non-zero on one rank).
-  --scaling weak: every rank renders a full 800x800 band of an 800 x 800N
+  --scaling strong (default): THE frame, its 16x16 tiles dealt to the ranks
+      round-robin; each rank renders 1/N of the pixels, and
+      the float4 framebuffer is summed to rank 0 with ONE reduce per step
+      (RCCL over xGMI), overlapped with the next step's render (two canvases,
+      alternating; exact: every pixel is non-zero on one rank).
+  --scaling weak: every rank renders a full nx x ny band of an nx x ny*N
       canvas (per-GPU work fixed).
 
 Rank 0 prints one JSON line.  `value` = all ranks' samples / max-over-ranks
@@ -41,6 +47,13 @@ sys.path.insert(0, ROOT)
 METRIC = "Msamples/sec (whole node), Cornell Box 800×800×1000spp; per-pixel RMSE vs ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 TILE = 16
+# BASELINE.json configs: the bench workloads and their committed oracle fixtures
+WORKLOADS = {
+    "c2": {"nx": 800, "ny": 800, "spp": 1000, "depth": 50, "golden": "c2_full.npz",
+           "name": "C2: Cornell Box 800x800, 1000 spp, depth 50"},
+    "c4": {"nx": 1920, "ny": 1080, "spp": 4096, "depth": 50, "golden": "c4_subset16k.npz",
+           "name": "C4: Cornell Box 1920x1080, 4096 spp, depth 50 (BASELINE configs[3], image-tile shard)"},
+}
 
 
 def cpu_baseline(budget_s: float, nx: int, ny: int, depth: int, nthreads: int = 1) -> dict:
@@ -100,29 +113,39 @@ def load_traffic(path: str, cfg: dict):
 
 
 def load_golden_frame(path: str):
-    """tests/golden/c2_full.npz (tools/make_golden.py full_frame_fixture): the
-    oracle's un-normalised rgb sums [N, 3] and its config, or None."""
+    """The oracle's committed fixture of the workload: tests/golden/c2_full.npz
+    (tools/make_golden.py full_frame_fixture, every pixel: un-normalised rgb
+    sums [N, 3]) or a pixel-subset fixture (c4_subset16k.npz: `pixels` and
+    their sums), with its config; None if absent."""
     try:
         z = np.load(path, allow_pickle=False)
     except OSError:
         return None
-    rgb = np.ascontiguousarray(z["rgb_planes"].T).view(np.float32).reshape(-1, 3)
-    return {"rgb": rgb, "nx": int(z["nx"]), "ny": int(z["ny"]), "spp": int(z["spp"]), "depth": int(z["depth"])}
+    if "rgb_planes" in z.files:
+        rgb, pixels = np.ascontiguousarray(z["rgb_planes"].T).view(np.float32).reshape(-1, 3), None
+    else:
+        rgb, pixels = np.asarray(z["rgb"], np.float32), np.asarray(z["pixels"], np.int64)
+        if int(z["seed_base"]) != 0:
+            return None
+    return {"rgb": rgb, "pixels": pixels, "nx": int(z["nx"]), "ny": int(z["ny"]), "spp": int(z["spp"]),
+            "depth": int(z["depth"])}
 
 
 def frame_quality(canvas: np.ndarray, gold: dict, spp: int) -> dict:
     """Per-pixel RMSE of the normalised frames (NormalizeFunctor, main.cc:253-287,
-    before quantisation) and bitwise equality of the sums (NaN-aware)."""
+    before quantisation) and bitwise equality of the sums (NaN-aware), over
+    every pixel the fixture holds (the whole frame, or its pixel subset)."""
     import raytracingtherestofyourlife_amd as rtp
 
-    a = np.ascontiguousarray(canvas, dtype=np.float32).copy()
+    a = np.ascontiguousarray(canvas if gold["pixels"] is None else canvas[gold["pixels"]], dtype=np.float32).copy()
     b = np.c_[gold["rgb"], np.zeros(len(gold["rgb"]), np.float32)].astype(np.float32)
     same = (a[:, :3].view(np.uint32) == b[:, :3].view(np.uint32)) | (np.isnan(a[:, :3]) & np.isnan(b[:, :3]))
     rtp.normalize(a, spp)
     rtp.normalize(b, spp)
     d = a[:, :3].astype(np.float64) - b[:, :3].astype(np.float64)
     return {"rmse": float(np.sqrt(np.mean(d * d))), "bit_exact": bool(same.all()),
-            "pixels_differing": int((~same.all(1)).sum()), "nan_pixels_ref": int(np.isnan(gold["rgb"]).any(1).sum())}
+            "pixels_checked": int(len(b)), "pixels_differing": int((~same.all(1)).sum()),
+            "nan_pixels_ref": int(np.isnan(gold["rgb"]).any(1).sum())}
 
 
 def load_valu(path: str, cfg: dict, kernel_ms: float):
@@ -154,10 +177,12 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="strong: the one 800x800 frame dealt over the ranks; weak: an 800x800 band per rank")
-    ap.add_argument("--nx", type=int, default=800)
-    ap.add_argument("--ny", type=int, default=800, help="rows of the frame (weak: per GPU, canvas nx x ny*N)")
-    ap.add_argument("--spp", type=int, default=1000)
-    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--workload", default="auto", choices=["auto", "c2", "c4"],
+                    help="auto: c2 on one GPU (the metric's frame), c4 on N > 1 (the tile-shard configuration)")
+    ap.add_argument("--nx", type=int, default=None, help="override the workload's width")
+    ap.add_argument("--ny", type=int, default=None, help="rows of the frame (weak: per GPU, canvas nx x ny*N)")
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--ff-tables", default="on", choices=["on", "auto", "off"],
                     help="RNG jump-table policy (include/rtp.h rtp_set_ff_tables); on: a long-lived renderer, "
                          "tables built during setup (reported in `setup`)")
@@ -167,9 +192,12 @@ def main() -> None:
                     help="nccl (RCCL over xGMI, production); gloo: host-side reduce, for rehearsing N>1 on one GPU")
     ap.add_argument("--share-gpu", action="store_true", help="every rank uses device 0 (rehearsal on a 1-GPU box)")
     ap.add_argument("--check", action="store_true", help="rank 0 verifies the reduced canvas against a 1-process render")
+    ap.add_argument("--force-collective", action="store_true",
+                    help="create the process group and run the per-step reduce even on one rank (torchrun "
+                         "--nproc-per-node 1: exercises the RCCL path on a one-GPU box)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c2.json"))
     ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "valu_c2.json"))
-    ap.add_argument("--golden", default=os.path.join(ROOT, "tests", "golden", "c2_full.npz"))
+    ap.add_argument("--golden", default=None, help="whole-frame fixture (c2) or pixel-subset fixture (c4)")
     args = ap.parse_args()
 
     import torch
@@ -183,13 +211,21 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    workload = args.workload if args.workload != "auto" else ("c2" if world == 1 else "c4")
+    W = WORKLOADS[workload]
+    for k in ("nx", "ny", "spp", "depth"):
+        if getattr(args, k) is None:
+            setattr(args, k, W[k])
+    if args.golden is None:
+        args.golden = os.path.join(ROOT, "tests", "golden", W["golden"])
     gpu = 0 if args.share_gpu else local
     torch.cuda.set_device(gpu)
-    if world > 1:
+    if world > 1 or args.force_collective:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         else:
             dist.init_process_group("gloo")
+    grouped = dist.is_initialized()
 
     strong = args.scaling == "strong"
     nx, ny = args.nx, args.ny * (1 if strong else world)
@@ -219,7 +255,7 @@ def main() -> None:
     # RCCL: the reduce of step k runs on the collective stream while step k+1
     # renders (shard.OverlappedCanvasReduce); gloo reduces host tensors.
     red = shard.OverlappedCanvasReduce(canvas, dist, overlap=(args.dist_backend == "nccl"),
-                                       host_copy=(args.dist_backend != "nccl"))
+                                       host_copy=(args.dist_backend != "nccl"), force=args.force_collective)
 
     def gather_canvas():
         return red.step(ids, out)
@@ -260,7 +296,7 @@ def main() -> None:
     live_total = int(live.to(torch.int64).sum().item())
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
+    if grouped:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -272,7 +308,7 @@ def main() -> None:
         canvas = gather_canvas()
     drain()
     torch.cuda.synchronize()
-    if world > 1:
+    if grouped:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if args.steps else float("nan")
@@ -306,7 +342,7 @@ def main() -> None:
         gold = load_golden_frame(args.golden)
         if gold and (gold["nx"], gold["ny"], gold["spp"], gold["depth"]) == (nx, ny, args.spp, args.depth):
             quality = frame_quality(canvas.cpu().numpy(), gold, args.spp)
-    if world > 1:
+    if grouped:
         t = torch.tensor([elapsed, live_total], dtype=torch.float64,
                          device="cuda" if args.dist_backend == "nccl" else "cpu")
         mx = t.clone()
@@ -346,10 +382,10 @@ def main() -> None:
             cpu = cpu_baseline(args.cpu_budget, args.nx, args.ny, args.depth)
         if world == 1 and args.cpu_budget_mt > 0:
             cpu_mt = cpu_baseline(args.cpu_budget_mt, args.nx, args.ny, args.depth, nthreads=host_threads())
-        if world == 1:
+        if world == 1 and not grouped:
             shard_desc = "one GPU: the whole frame"
         else:
-            shard_desc = (f"{TILE}x{TILE} tiles round-robin over {world} ranks, 1 "
+            shard_desc = (f"{TILE}x{TILE} tiles round-robin over {world} rank(s), 1 "
                           + ("RCCL" if args.dist_backend == "nccl" else "gloo") + " reduce/step")
         line = {
             "metric": METRIC,
@@ -366,12 +402,12 @@ def main() -> None:
             "data": "synthetic: the reference's deterministic Cornell Box scene and camera (main.cc:616-622), "
                     "seed = pixel index",
             "config": {
-                "workload": "C2: Cornell Box 800x800, 1000 spp, depth 50" + ("" if strong or world == 1 else
-                                                                          f" per GPU (canvas {nx}x{ny})"),
+                "workload": W["name"] + ("" if strong or world == 1 else f" per GPU (canvas {nx}x{ny})"),
                 "nx": nx, "ny": ny, "spp": args.spp, "depth": args.depth,
                 "pixels_per_gpu": npix,
                 "shard": shard_desc + (" (pixel of each tile entry computed in-kernel)" if tiled else " (pixel list)"),
                 "live_bounces_per_sample": round(L, 6),
+                "dist_backend": args.dist_backend if grouped else None,
             },
             "rmse": None if quality is None else quality["rmse"],
             "bit_exact": None if quality is None else quality["bit_exact"],
@@ -406,7 +442,7 @@ def main() -> None:
         if check is not None:
             line["check_reduced_canvas_equals_single_render"] = check
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if grouped:
         dist.destroy_process_group()
 
 

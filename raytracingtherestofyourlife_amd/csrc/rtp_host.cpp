@@ -255,19 +255,12 @@ void ff_auto_samples(uint64_t& chain, uint64_t& direct) {
   }
 }
 
-void ff_free(FfTables& T) {
-  for (uint32_t*& p : T.t) {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-  }
-  if (T.direct) (void)hipFree(T.direct);
-  T.direct = nullptr;
-  T.d_count = T.n_chain = 0;
-  T.bytes = 0;
-}
-
 // Allocate and build the tables of a device up to `stage` (caller holds
-// g_ff_mu): 1 the chain tables, 2 also the direct block.
+// g_ff_mu): 1 the chain tables, 2 also the direct block.  The new tables are
+// allocated and built through local pointers and published into T only once
+// the build kernel has finished: a launch that took its snapshot (FfSnap)
+// earlier, and may still be running on another stream, never sees a table
+// that is half built, and a failed build frees only what it allocated.
 void ff_build(FfTables& T, int stage) {
   if (T.stage >= stage) return;
   int want = 4, nd = 10, first = 41;
@@ -282,16 +275,19 @@ void ff_build(FfTables& T, int stage) {
     return hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b >= n + reserve;
   };
   rtp::FfBuildOut out{};
+  uint32_t* chain[rtp::kFfTables] = {};
+  uint32_t* direct = nullptr;
+  int n_chain = 0, d_count = 0;
   int max_r = 0;
   const auto t0 = std::chrono::steady_clock::now();
   if (T.stage < 1) {
     for (int j = 0; j < want; j++) {
-      if (!fits(bytes) || hipMalloc(&T.t[j], bytes) != hipSuccess) {
-        T.t[j] = nullptr;
+      if (!fits(bytes) || hipMalloc(&chain[j], bytes) != hipSuccess) {
+        chain[j] = nullptr;
         break;
       }
-      T.n_chain = j + 1;
-      out.t[32 >> j] = T.t[j];
+      n_chain = j + 1;
+      out.t[32 >> j] = chain[j];
       max_r = std::max(max_r, 32 >> j);
     }
   }
@@ -301,20 +297,19 @@ void ff_build(FfTables& T, int stage) {
       nd = std::min<int>(nd, free_b > reserve ? (int)((free_b - reserve) / bytes) : 0);
     else
       nd = 0;
-    if (nd > 0 && hipMalloc(&T.direct, bytes * (size_t)nd) == hipSuccess) {
-      T.d_first = first;
-      T.d_count = nd;
+    if (nd > 0 && hipMalloc(&direct, bytes * (size_t)nd) == hipSuccess) {
+      d_count = nd;
       for (int k = 0; k < nd; k++) {
-        out.t[first + k] = T.direct + (size_t)k * (bytes / 4);
+        out.t[first + k] = direct + (size_t)k * (bytes / 4);
         max_r = std::max(max_r, first + k);
       }
     } else {
-      T.direct = nullptr;
+      direct = nullptr;
     }
   }
   (void)hipGetLastError();
   T.alloc_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  T.stage = stage;
+  T.stage = stage;  // (a failed stage is not retried)
   if (max_r > 0) {
     const uint32_t t1 = which_threshold(2), t2 = which_threshold(3);
     hipEvent_t a = nullptr, b = nullptr;
@@ -327,18 +322,37 @@ void ff_build(FfTables& T, int stage) {
     if (a) (void)hipEventDestroy(a);
     if (b) (void)hipEventDestroy(b);
     (void)hipGetLastError();
-    if (!ok) {
-      ff_free(T);
+    if (!ok) {  // nothing was published: free this stage's own allocations
+      for (uint32_t* p : chain)
+        if (p) (void)hipFree(p);
+      if (direct) (void)hipFree(direct);
       return;
     }
     T.build_ms += ms;
   }
+  // publish (the build has completed)
+  for (int j = 0; j < n_chain; j++) T.t[j] = chain[j];
+  if (n_chain > 0) T.n_chain = n_chain;
+  if (d_count > 0) {
+    T.direct = direct;
+    T.d_first = first;
+    T.d_count = d_count;
+  }
   T.bytes = bytes * (size_t)(T.n_chain + T.d_count);
 }
 
+// What one launch reads of a device's tables: a copy taken under g_ff_mu,
+// so a later stage being built by another thread cannot change it.
+struct FfSnap {
+  const uint32_t* t[rtp::kFfTables] = {};
+  const uint32_t* direct = nullptr;
+  int d_first = 0, d_count = 0;
+};
+
 // The tables a launch of `samples` samples on `device` uses under `policy`
-// (built first when the policy says so).
-const FfTables& ff_tables(int device, int policy, uint64_t samples) {
+// (built first when the policy says so).  The tables, once published, stay
+// until the process ends.
+FfSnap ff_tables(int device, int policy, uint64_t samples) {
   std::lock_guard<std::mutex> lk(g_ff_mu);
   FfTables& T = g_ff[device & 63];
   T.samples_seen += samples;
@@ -350,8 +364,13 @@ const FfTables& ff_tables(int device, int policy, uint64_t samples) {
     if (T.samples_seen >= direct) ff_build(T, 2);
     else if (T.samples_seen >= chain) ff_build(T, 1);
   }
-  static const FfTables none{};
-  return policy == RTP_FF_TABLES_OFF ? none : T;
+  FfSnap s;
+  if (policy == RTP_FF_TABLES_OFF) return s;
+  for (int j = 0; j < rtp::kFfTables; j++) s.t[j] = T.t[j];
+  s.direct = T.direct;
+  s.d_first = T.d_first;
+  s.d_count = T.d_count;
+  return s;
 }
 
 // Sphere BVH (replaces the VTK-m LinearBVH of buildBVH, MapperPathTracer.cxx:
@@ -959,7 +978,7 @@ rtp_status check_render_args(rtp_context* c, const rtp_camera* cam, int32_t nx, 
   // device-side bookkeeping limits: the pool kernel packs the remaining dead
   // depths into 14 bits and counts a wave's finished samples (<= 256 * spp)
   // in 32-bit signed cursors
-  if (depth > rtp::kMaxDepth) return fail(RTP_ERR_INVALID_ARGUMENT, "render: depthcount must be <= 8191");
+  if (depth > rtp::kMaxDepth) return fail(RTP_ERR_INVALID_ARGUMENT, "render: depthcount must be <= 16383");
   if (spp > rtp::kMaxSpp) return fail(RTP_ERR_INVALID_ARGUMENT, "render: samplecount must be <= 8388607");
   return RTP_OK;
 }
@@ -1027,7 +1046,7 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
   p.dbg = nullptr;
   p.progress = c->d_progress;
   if (variant == 2) {
-    const FfTables& ft = ff_tables(c->device, c->ff_policy, (uint64_t)npix * (uint64_t)spp);
+    const FfSnap ft = ff_tables(c->device, c->ff_policy, (uint64_t)npix * (uint64_t)spp);
     for (int j = 0; j < rtp::kFfTables; j++) p.ff[j] = ft.t[j];
     p.ffd = ft.direct, p.ffd_first = ft.d_first, p.ffd_count = ft.d_count;
   }
@@ -1176,6 +1195,18 @@ rtp_status rtp_render_planned_device(rtp_context* c, const rtp_camera* cam, int3
     return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_render_planned_device: bad plan / output");
   if (!d_pixel_ids && (pixel_begin < 0 || pixel_begin + pixel_count > (int64_t)nx * ny))
     return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_render_planned_device: pixel range outside the canvas");
+  {  // the plan must cover [0, pixel_count) exactly, in order, <= 128 entries per wave (one pool)
+    HIP_TRY(hipSetDevice(c->device));
+    std::vector<int32_t> plan((size_t)n_waves + 1);
+    HIP_TRY(hipMemcpyAsync(plan.data(), d_wave_begin, plan.size() * sizeof(int32_t), hipMemcpyDeviceToHost,
+                           (hipStream_t)hip_stream));
+    HIP_TRY(hipStreamSynchronize((hipStream_t)hip_stream));
+    bool ok = plan[0] == 0 && plan[n_waves] == pixel_count;
+    for (int32_t w = 0; ok && w < n_waves; w++) ok = plan[w] <= plan[w + 1] && plan[w + 1] - plan[w] <= rtp::kPoolSlots;
+    if (!ok)
+      return fail(RTP_ERR_INVALID_ARGUMENT,
+                  "rtp_render_planned_device: wave_begin must rise from 0 to pixel_count in steps of at most 128");
+  }
   double ms = 0;
   rs = launch(c, cam, nx, ny, spp, depth, seed_base, pixel_begin, pixel_count, d_pixel_ids, d_rgba_out,
               aux ? aux->final_seed : nullptr, aux ? aux->live_bounces : nullptr, (hipStream_t)hip_stream,
@@ -1249,7 +1280,7 @@ rtp_status rtp_eval_primitive(rtp_context* c, int32_t kind, const void* in, void
   HIP_TRY(hipSetDevice(c->device));
   const uint32_t* tab = nullptr;
   if (kind == 4 || kind == 5 || kind == 7) {
-    const FfTables& ft = ff_tables(c->device, c->ff_policy, 0);
+    const FfSnap ft = ff_tables(c->device, c->ff_policy, 0);
     tab = kind == 4 ? ft.t[1] : kind == 5 ? ft.t[0] : ft.direct;  // 16 / 32 dead depths, direct_first
     if (!tab) return fail(RTP_ERR_DEVICE, "rtp_eval_primitive: RNG jump tables are not built (policy or memory)");
   }

@@ -867,6 +867,7 @@ constexpr int kWavesPerBlock = 4;
 #define RTP_POOL 128
 #endif
 constexpr int kPool = RTP_POOL;  // pixel slots per wave (power of two: queue index = cursor & (kPool-1))
+static_assert(kPool == kPoolSlots || RTP_POOL != 128, "rtp_layout.hpp kPoolSlots is the production pool size");
 static_assert((kPool & (kPool - 1)) == 0 && kPool >= 64, "pool size must be a power of two >= 64");
 // LDS per wave: seed, r, g, b, samples, live (u32) + rem, q_ready, q_ff (u16):
 // 30 B x 128 slots x 4 waves + the 2 KB quad shading table = 17 KiB per
@@ -983,9 +984,9 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
   // slot j of wave w <-> list entry k = j * n_waves + w (pixels interleaved over waves)
   // or, planned, k = wave_begin[w] + j
   int n_slots, wbase = 0;
-  if constexpr (kPlan) {
+  if constexpr (kPlan) {  // (the host checked the plan; the clamps keep a bad one inside the buffers)
     wbase = p.wave_begin[w];
-    n_slots = min(kPool, p.wave_begin[w + 1] - wbase);
+    n_slots = max(0, min(min(kPool, p.wave_begin[w + 1] - wbase), (int)(p.npix - wbase)));
   } else {
     const int64_t left = p.npix - w;
     n_slots = left <= 0 ? 0 : (int)min<int64_t>(kPool, (left + n_waves - 1) / n_waves);
@@ -1004,7 +1005,11 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
   }
   wave_sync();
   // wave-uniform, monotone queue cursors
-  int ready_head = 0, ready_tail = (S > 0) ? n_slots : 0, ff_head = 0, ff_tail = 0;
+  // (uint32: under kSteal a wave's finished-sample count ff_tail runs over
+  // every pixel it claims -- C5 on one GPU: ~2.6e10 -- so it wraps; only the
+  // differences of cursors (each < 2^31: <= kPool * spp) and their low bits
+  // (the ring index) are used, and unsigned arithmetic wraps exactly)
+  uint32_t ready_head = 0, ready_tail = (S > 0) ? n_slots : 0, ff_head = 0, ff_tail = 0;
   int unfinished = n_slots;                // stats only: pixels with samples still to run
   unsigned long long t_tail = 0;
 
@@ -1030,10 +1035,11 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
         (unsigned)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));  // HW_REG_HW_ID
   }
 
-  int published = 0;  // wave-uniform: finished samples already added to p.progress
+  uint32_t published = 0;  // wave-uniform: ff_tail when the finished samples were last added to p.progress
   // kSteal (wave-uniform): slots still holding a pixel, and the samples of the
   // pixels already written out (the fair-share average is over the others)
-  int live_slots = n_slots, retired = 0;
+  int live_slots = n_slots;
+  uint32_t retired = 0;  // (the samples of the written-out pixels, mod 2^32 like ff_tail)
   bool critical_ff = false;  // wave-uniform: a critical (far-lagging) pixel waits in the FF queue
 
   bool has_path = false;
@@ -1059,8 +1065,8 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
   for (;;) {
     const uint64_t idle = __ballot(!has_path);
     const int n_idle = __popcll(idle);
-    const int n_ready = ready_tail - ready_head;
-    const int n_ff = ff_tail - ff_head;
+    const int n_ready = (int)(ready_tail - ready_head);
+    const int n_ff = (int)(ff_tail - ff_head);
     if ((n_ready < n_idle + RTP_FF_MARGIN || critical_ff) && n_ff > 0) {
       critical_ff = false;
       // ---- batch RNG fast-forward over the remaining dead depths of finished
@@ -1182,7 +1188,7 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
           unsigned long long base = 0;
           if (lane == 0) base = atomicAdd(kparams().progress + 1, (unsigned long long)nd);
           base = __shfl(base, 0) + (unsigned long long)n_waves * kPool;
-          retired += nd * S;
+          retired += (uint32_t)(nd * S);
           if (mine && !again) {
             const int64_t k = (int64_t)s_entry[fslot];
             reinterpret_cast<float4*>(p.out)[k] = make_float4(s_r[fslot], s_g[fslot], s_b[fslot], 0.f);
@@ -1210,13 +1216,14 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
       // paths, back sooner) take more than their share of lanes, so the
       // expensive pixels' sequential sample chains ran on alone at the end
       // (17% of bounce steps with ~12 of 64 lanes live).
-      // (samples * n_slots <= 2^23 * 2^8 and ff_tail <= n_slots * spp: 32 bits suffice)
+      // (samples * slots <= 2^23 * 2^7; ff_tail (no stealing) and ff_tail - retired (the
+      // held pixels' finished samples) are <= 2^7 * spp: 32 bits suffice)
       const bool urgent = again && (kSteal ? s_samples[fslot] * (uint32_t)live_slots <= (uint32_t)(ff_tail - retired)
                                            : s_samples[fslot] * (uint32_t)n_slots <= (uint32_t)ff_tail);
       const uint64_t pu = __ballot(urgent), pn = __ballot(again && !urgent);
-      ready_head -= __popcll(pu);
-      if (urgent) q_ready[(ready_head + (int)lane_rank(pu)) & (kPool - 1)] = (uint16_t)fslot;
-      if (again && !urgent) q_ready[(ready_tail + (int)lane_rank(pn)) & (kPool - 1)] = (uint16_t)fslot;
+      ready_head -= (uint32_t)__popcll(pu);
+      if (urgent) q_ready[(ready_head + lane_rank(pu)) & (kPool - 1)] = (uint16_t)fslot;
+      if (again && !urgent) q_ready[(ready_tail + lane_rank(pn)) & (kPool - 1)] = (uint16_t)fslot;
       ready_tail += __popcll(pn);
       ff_head += n;
       wave_sync();
@@ -1232,7 +1239,7 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
     }
     // ---- refill idle lanes with the next sample of READY pixels ----
     const unsigned long long tb = stamp(want_dbg);
-    const int take = min(n_idle, ready_tail - ready_head);
+    const int take = min(n_idle, (int)(ready_tail - ready_head));
     if (!has_path) {
       const int r = (int)lane_rank(idle);
       if (r < take) {
@@ -1326,7 +1333,7 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
       dbg[kDbgCyclesEnd] += te - tbnc;
     }
     const uint64_t fin = __ballot(ended);
-    if (ended) q_ff[(ff_tail + (int)lane_rank(fin)) & (kPool - 1)] = (uint16_t)slot;
+    if (ended) q_ff[(ff_tail + lane_rank(fin)) & (kPool - 1)] = (uint16_t)slot;
 #if RTP_CRIT_FF > 0
     // A pixel whose finished samples lag the wave's average by more than
     // RTP_CRIT_FF/1000 runs its sample chain on the critical path (its path
@@ -1340,14 +1347,26 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
 #endif
     ff_tail += __popcll(fin);
     wave_sync();
-    if (RTP_PRIO_BALANCE && ff_tail - published >= kPrioPeriod) {
-      // ff_tail counts this wave's finished samples
+    if (RTP_PRIO_BALANCE && ff_tail - published >= (uint32_t)kPrioPeriod) {
       unsigned long long g = 0;
       if (lane == 0) g = atomicAdd(kparams().progress, (unsigned long long)(ff_tail - published));
       g = __shfl(g, 0) + (unsigned long long)(ff_tail - published);
       published = ff_tail;
-      // completed fractions: global g / (npix*S) vs own ff_tail / (n_slots*S)
-      float lag = ((float)g / (float)kparams().npix - (float)ff_tail / (float)n_slots) / (float)S;
+      float lag;
+      if constexpr (kSteal) {
+        // remaining samples: this wave's (its held pixels') against the
+        // average wave's, npix * S - g over the waves.  While unclaimed
+        // entries remain, the average includes them and every wave sits
+        // below it (priority 0: the stealing balances); once they are gone
+        // the waves with the most work left get the issue slots.  In units
+        // of a full pool's samples, like the fractions below.
+        const float mine_left = (float)live_slots * (float)S - (float)(ff_tail - retired);
+        const float avg_left = ((float)kparams().npix * (float)S - (float)g) / (float)n_waves;
+        lag = (mine_left - avg_left) / ((float)kPool * (float)S);
+      } else {
+        // completed fractions: global g / (npix*S) vs own ff_tail / (n_slots*S)
+        lag = ((float)g / (float)kparams().npix - (float)ff_tail / (float)n_slots) / (float)S;
+      }
       set_priority(lag);
     }
     if (want_dbg && unfinished < 64) {
@@ -1605,13 +1624,42 @@ extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int bvh, int* variant_ou
   return W * rtp::kPool;
 }
 
+// Waves of the stealing instances that fit the chip at once: their own
+// occupancy (the s_entry table adds 2 KiB of LDS per block), the smaller of
+// the contiguous / pixel-list and tile-deal instances.  A stealing launch
+// larger than this would leave blocks waiting for a free CU, and their
+// statically assigned first entries would run as a tail after the stolen work.
+namespace {
+template <bool kBvh>
+int steal_blocks_per_cu() {
+  int a = 0, b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, rtp::rtp_render_pool<false, kBvh, false, false, true>, 256, 0) !=
+          hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtp::rtp_render_pool<false, kBvh, true, false, true>, 256, 0) !=
+          hipSuccess)
+    return 1;
+  return std::max(1, std::min(a, b));
+}
+int steal_resident_waves(int bvh) {
+  static int cached[2] = {-1, -1};
+  int& c = cached[bvh ? 1 : 0];
+  if (c > 0) return c;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 1024;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  c = cus * (bvh ? steal_blocks_per_cu<true>() : steal_blocks_per_cu<false>()) * rtp::kWavesPerBlock;
+  return c;
+}
+}  // namespace
+
 // Work stealing (pool_body kSteal) when a launch's entries exceed what the
 // resident waves' pools hold: the resident waves, each refilling its slots
 // from the unclaimed entries.  Returns the waves (0: no stealing).
 extern "C" int rtp_plan_steal(int64_t npix, int bvh) {
   if (bvh == 2) return 0;  // (the LDS walk's kernel has no stealing instance)
   const int64_t resident = pool_resident_waves(false, bvh);
-  return npix > resident * rtp::kPool ? (int)resident : 0;
+  if (npix <= resident * rtp::kPool) return 0;
+  return std::min<int>((int)resident, steal_resident_waves(bvh));
 }
 
 extern "C" hipError_t rtp_launch_eval_closest(const rtp::DevScene* scene, const float* rays, uint32_t* out,

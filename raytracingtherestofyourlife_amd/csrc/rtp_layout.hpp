@@ -12,8 +12,9 @@
 namespace rtp {
 
 constexpr int kMaxQuads = 256;
-constexpr int kMaxDepth = 8191;     // remaining dead depths fit the 13-bit field of the pool's slots
-constexpr int kMaxSpp = 8388607;    // 256 slots * spp fits the pool's 32-bit sample cursors
+constexpr int kMaxDepth = 16383;    // remaining dead depths fit the 14-bit field of the pool's slots (kRemMask)
+constexpr int kMaxSpp = 8388607;    // 256 slots * spp fits the pool's 32-bit sample cursors (kSteal: see pool_body)
+constexpr int kPoolSlots = 128;  // pixel slots per persistent wave of the pool kernel (a planned wave's range bound)
 constexpr int kMaxSpheres = 256;          // held inline in DevScene (scalar loads)
 constexpr int kMaxSpheresBvh = 1 << 22;   // spheres behind the BVH (global memory)
 constexpr int kBvhMinSpheres = 9;         // scenes with more spheres use the BVH

@@ -95,15 +95,17 @@ class OverlappedCanvasReduce:
     reduce (async) runs while the next step renders; a canvas is reused only
     after its reduce has been waited on.  overlap=False: one canvas, a
     synchronous reduce (gloo reduces host tensors: `host_copy` moves a device
-    canvas through the host)."""
+    canvas through the host).  force: run the collective even on one rank
+    (a world-size-1 RCCL group exercises the same calls on a one-GPU box)."""
 
-    def __init__(self, canvas, dist, overlap: bool, host_copy: bool = False):
+    def __init__(self, canvas, dist, overlap: bool, host_copy: bool = False, force: bool = False):
         import torch
 
         self.dist, self.overlap, self.host_copy = dist, overlap, host_copy
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.rank = dist.get_rank() if dist.is_initialized() else 0
-        self.canvases = [canvas, torch.zeros_like(canvas)] if overlap and self.world > 1 else [canvas]
+        self.collective = dist.is_initialized() and (self.world > 1 or force)
+        self.canvases = [canvas, torch.zeros_like(canvas)] if overlap and self.collective else [canvas]
         self.pending = [None] * len(self.canvases)
         self.steps = 0
 
@@ -118,7 +120,7 @@ class OverlappedCanvasReduce:
         c = self.canvases[slot]
         c.zero_()
         c.index_copy_(0, ids, part)
-        if self.world > 1:
+        if self.collective:
             if len(self.canvases) > 1:
                 self.pending[slot] = self.dist.reduce(c, dst=0, op=self.dist.ReduceOp.SUM, async_op=True)
             elif self.host_copy:

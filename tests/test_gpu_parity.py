@@ -216,9 +216,20 @@ def test_invalid_arguments(device, rtp):
     with pytest.raises(rtp.RtpError):
         device.render_pixels(cam, 4, 4, 1, 1, np.array([16], dtype=np.int64))
     with pytest.raises(rtp.RtpError):  # device bookkeeping limits (rtp_layout.hpp kMaxDepth / kMaxSpp)
-        device.render(cam, 4, 4, 1, 8192)
+        device.render(cam, 4, 4, 1, 16384)
     with pytest.raises(rtp.RtpError):
         device.render(cam, 4, 4, 8388608, 1)
+
+
+def test_depth_at_the_bookkeeping_limit(oracle, device, rtp):
+    """depthcount up to kMaxDepth = 16383 (s_rem's 14-bit count field): a
+    deep render of a few pixels equals the oracle's, final seeds and
+    live-bounce counts included (almost every depth is a dead one, so the
+    fast-forward runs its full chain of jump tables and hashed steps)."""
+    nx, ny = 6, 4
+    pix = np.arange(nx * ny, dtype=np.int64)
+    got, want = _render_both(oracle, device, rtp, 0, nx, ny, 3, 16383, pix)
+    assert_render_equal(got, want, "depth 16383")
 
 
 def test_empty_pixel_list_and_zero_spp(device, rtp):

@@ -1,0 +1,81 @@
+"""C5's sample-batch shard (shard.sample_batches: rank k renders spp/G samples
+of every pixel from seed = pixel + k*N) is a derived stream, not the
+reference's.  Two checks: (a) exact against the oracle on
+the same schedule (tests/golden c5_shard3_*, test_shard.py); (b) here,
+statistical against the unsharded stream (seeds[i] = i, MapperPathTracer.cxx:
+265-267): the sharded image and the single-stream image must agree within
+Monte Carlo noise, before and after NormalizeFunctor (main.cc:253-287).  The
+noise is measured from the spread of the G shards themselves
+(_util.sample_shard_consistency)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from _util import assert_shards_consistent, sample_shard_consistency
+
+
+def test_oracle_sample_shards_match_single_stream_statistically(oracle):
+    """CPU, the checker: a 64x36 frame (C5's aspect) at 256 spp, depth 50, 8 shards."""
+    from raytracingtherestofyourlife_amd import shard
+
+    nx, ny, spp, depth, G = 64, 36, 256, 50, 8
+    sc = oracle.cornell_box(0)
+    cam = oracle.camera_setup(nx, ny)
+    pix = np.arange(nx * ny, dtype=np.int64)
+    single = oracle.render_pixels(sc, cam, nx, ny, spp, depth, pix, nthreads=0)[0]
+    shards = [oracle.render_pixels(sc, cam, nx, ny, b.spp, depth, pix, seed_base=b.seed_base, nthreads=0)[0]
+              for b in shard.sample_batches(spp, G, nx * ny)]
+    st = sample_shard_consistency(single, shards, spp)
+    assert_shards_consistent(st, "oracle 64x36x256")
+    # and the summed shards are not the single stream (a derived stream, not a copy of it)
+    assert not np.array_equal(single[:, :3], np.sum(shards, axis=0)[:, :3])
+
+
+def test_shard_consistency_detects_a_biased_image(oracle):
+    """The check has power: a sharded image scaled by 2% (a biased estimator)
+    or rendered at the wrong depth fails it."""
+    from raytracingtherestofyourlife_amd import shard
+
+    nx, ny, spp, depth, G = 64, 36, 256, 50, 8
+    sc = oracle.cornell_box(0)
+    cam = oracle.camera_setup(nx, ny)
+    pix = np.arange(nx * ny, dtype=np.int64)
+    single = oracle.render_pixels(sc, cam, nx, ny, spp, depth, pix, nthreads=0)[0]
+    batches = shard.sample_batches(spp, G, nx * ny)
+    shards = [oracle.render_pixels(sc, cam, nx, ny, b.spp, depth, pix, seed_base=b.seed_base, nthreads=0)[0]
+              for b in batches]
+    with pytest.raises(AssertionError):
+        assert_shards_consistent(sample_shard_consistency(single, [s * 1.02 for s in shards], spp))
+    shallow = [oracle.render_pixels(sc, cam, nx, ny, b.spp, 2, pix, seed_base=b.seed_base, nthreads=0)[0]
+               for b in batches]
+    with pytest.raises(AssertionError):
+        assert_shards_consistent(sample_shard_consistency(single, shallow, spp))
+
+
+@pytest.mark.gpu
+def test_hip_sample_shards_match_single_stream_statistically(device):
+    """GPU: a 256x144 frame (C5's aspect, 1/225 of its pixels) at 2048 spp,
+    depth 50, 8 sample shards on the device path bench/render_dist use."""
+    import torch
+
+    import raytracingtherestofyourlife_amd as rtp
+    from raytracingtherestofyourlife_amd import shard
+
+    nx, ny, spp, depth, G = 256, 144, 2048, 50, 8
+    n = nx * ny
+    cam = rtp.default_camera()
+    s = torch.cuda.current_stream().cuda_stream
+    device.set_cornell_box(0)
+
+    def render(k_spp, seed_base):
+        out = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
+        device.render_device(cam, nx, ny, k_spp, depth, out.data_ptr(), seed_base=seed_base, stream=s)
+        torch.cuda.synchronize()
+        return out.cpu().numpy()
+
+    single = render(spp, 0)
+    shards = [render(b.spp, b.seed_base) for b in shard.sample_batches(spp, G, n)]
+    st = sample_shard_consistency(single, shards, spp)
+    assert_shards_consistent(st, "hip 256x144x2048")
+    assert st["n"] > 0.99 * n

@@ -18,8 +18,15 @@ ap.add_argument("--rank", type=int, default=0, help="--tiles: the rank whose sha
 ap.add_argument("--ff-tables", default="on", choices=["on", "auto", "off"], help="RNG jump-table policy")
 ap.add_argument("--list-tiles", action="store_true", help="the pixel-list path over the tile deal's order")
 ap.add_argument("--list-contig", action="store_true", help="the pixel-list path over the contiguous order")
+ap.add_argument("--share", action="store_true",
+                help="the pixel-list path over rank --rank's tiles of the --world deal (shard.tile_pixels: any canvas, "
+                     "clipped edge tiles; bench.py's path for canvases that are not whole tiles, e.g. C4's 1080 rows)")
+ap.add_argument("--seed-base", type=int, default=0)
 a = ap.parse_args()
 ids = None
+if a.share:
+    from raytracingtherestofyourlife_amd import shard
+    ids = torch.from_numpy(shard.tile_pixels(a.nx, a.ny, a.rank, a.world)).cuda()
 if a.list_contig:
     ids = torch.arange(a.nx * a.ny, dtype=torch.int64, device="cuda")
 if a.list_tiles:
@@ -29,7 +36,7 @@ dev = rtp.Device(0)
 dev.set_cornell_box(a.variant)
 dev.set_ff_tables(a.ff_tables)
 cam = rtp.default_camera()
-n = a.nx * a.ny
+n = a.nx * a.ny if ids is None else int(ids.numel())
 out = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
 live = torch.zeros(n, dtype=torch.int32, device="cuda")
 s = torch.cuda.current_stream().cuda_stream
@@ -37,18 +44,18 @@ for r in range(a.reps):
     t = time.time()
     if ids is not None:
         st = dev.render_device(cam, a.nx, a.ny, a.spp, a.depth, out.data_ptr(), pixel_count=n, pixel_ids_ptr=ids.data_ptr(),
-                               stream=s, live_ptr=live.data_ptr(), timed=True)
+                               stream=s, live_ptr=live.data_ptr(), timed=True, seed_base=a.seed_base)
     elif a.tiles:
         st = dev.render_tiles_device(cam, a.nx, a.ny, a.spp, a.depth, out.data_ptr(), a.rank, a.world, stream=s,
                                      timed=True)
     else:
         st = dev.render_device(cam, a.nx, a.ny, a.spp, a.depth, out.data_ptr(), stream=s, live_ptr=live.data_ptr(),
-                               timed=True)
+                               timed=True, seed_base=a.seed_base)
     torch.cuda.synchronize()
     wall = time.time() - t
     L = live.to(torch.int64).sum().item() / (n * a.spp)
     Lp = (live.to(torch.float64) / a.spp).cpu().numpy()
-    nr = n // a.world if a.tiles else n
-    print(json.dumps(dict(rep=r, kernel_ms=st.kernel_ms, wall_s=wall, msamples_per_s=nr * a.spp / (st.kernel_ms / 1e3) / 1e6,
+    nr = n // a.world if a.tiles else n  # (--share: n is already the rank's pixels)
+    print(json.dumps(dict(rep=r, npix=nr, kernel_ms=st.kernel_ms, wall_s=wall, msamples_per_s=nr * a.spp / (st.kernel_ms / 1e3) / 1e6,
                           live_per_sample=L, nan_px=int(torch.isnan(out[:, :3]).any(1).sum().item()),
                           L_pixel_pct={q: round(float(np.percentile(Lp, q)), 3) for q in (50, 90, 99, 99.9, 100)})), flush=True)
