@@ -594,6 +594,19 @@ enum BounceResult { kAlive = 0, kMissed = 1, kLight = 2 };
 // exactly the reference's draws for this depth and stores A[d] at hist_d
 // (when d <= D-2).  On kLight, `emit` receives E[d].
 RTP_DEV unsigned long long stamp(bool on) { return on ? __builtin_amdgcn_s_memtime() : 0ull; }
+// Stats build only (RTP_DEBUG_STATS=1): counters updated from divergent code
+// go straight to the wave's record in global memory (gdbg = p.dbg + wave *
+// kDbgCounters, zeroed before the launch), from its first active lane.
+// dbg_region: one visit and the lanes active at the region's start;
+// dbg_add: the sum of v over the active lanes.
+RTP_DEV void dbg_region(unsigned long long* gdbg, int c) {
+  const uint64_t m = __ballot(true);
+  if ((int)(threadIdx.x & 63) == (int)__builtin_ctzll(m)) {
+    atomicAdd(gdbg + c, 1ull);
+    atomicAdd(gdbg + c + 1, (unsigned long long)__popcll(m));
+  }
+}
+RTP_DEV void dbg_add(unsigned long long* gdbg, int c, unsigned long long v) { atomicAdd(gdbg + c, v); }
 
 // kDeferDead: a path that misses or hits the light at depth k leaves its
 // depth-k draws (which + generator, exactly one dead step) to the caller's
@@ -601,10 +614,11 @@ RTP_DEV unsigned long long stamp(bool on) { return on ? __builtin_amdgcn_s_memti
 // qshade: the block's LDS quad table (fill_qshade).
 template <bool kBvh, bool kDeferDead>
 RTP_DEV int shade_hit(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3& emit, float4* __restrict__ hist_d,
-                      int D, const float* qshade, const Hit h);
+                      int D, const float* qshade, const Hit h, unsigned long long* dbg = nullptr);
 template <bool kBvh, bool kDeferDead = false, bool kLdsBvh = false>
 RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3& emit, float4* __restrict__ hist_d,
-                   int D, unsigned long long* dbg, const float* qshade, const LdsBvhNode* lds_bvh = nullptr) {
+                   int D, unsigned long long* dbg, const float* qshade, const LdsBvhNode* lds_bvh = nullptr,
+                   unsigned long long* gdbg = nullptr) {
   const bool st = dbg != nullptr;
   const unsigned long long t0 = stamp(st);
   const f3 org = ps.org, dir = ps.dir;
@@ -620,15 +634,16 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
     const unsigned long long t1s = __builtin_amdgcn_s_memtime();
     dbg[kDbgCyclesIntersect] += t1s - t0;
   }
-  return shade_hit<kBvh, kDeferDead>(sc, ps, seed, emit, hist_d, D, qshade, h);
+  return shade_hit<kBvh, kDeferDead>(sc, ps, seed, emit, hist_d, D, qshade, h, gdbg);
 }
 
 // The rest of one depth once the closest hit h is known: collect, material,
 // generate, pdfs, scatter (bounce() above; the pool kernel's resumable
 // sphere-BVH walk calls it directly for the lanes whose walk has finished).
+// dbg (stats build only): the wave's global counter record (dbg_region).
 template <bool kBvh, bool kDeferDead>
 RTP_DEV int shade_hit(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3& emit, float4* __restrict__ hist_d,
-                      int D, const float* qshade, const Hit h) {
+                      int D, const float* qshade, const Hit h, unsigned long long* dbg) {
   const uint32_t t1 = sc->which_t1, t2 = sc->which_t2;
   const DevLights& L = sc->light;
   const f3 org = ps.org, dir = ps.dir;
@@ -637,6 +652,7 @@ RTP_DEV int shade_hit(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed,
     if (!kDeferDead) seed = dead_step(seed, t1, t2);  // which + generator draws of the now-dead ray
     return kMissed;
   }
+  if (dbg) dbg_region(dbg, kDbgHitVisits);
   f3 hp = add(org, scl(dir, h.t));
   f3 hn;
   int mt;
@@ -658,12 +674,15 @@ RTP_DEV int shade_hit(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed,
   }
   // applyMaterials (EmitWorklet.h)
   if (mt == 1) {  // DiffuseLightWorklet: emit, path ends (status &= 0)
+    if (dbg) dbg_region(dbg, kDbgLightVisits);
     emit = (dot(hn, dir) < 0.0f) ? alb : mk(0.f, 0.f, 0.f);
     if (!kDeferDead) seed = dead_step(seed, t1, t2);
     return kLight;
   }
   f3 atten;
   if (mt == 2) {  // DielectricWorklet: 1 draw before generation, specular
+    const unsigned long long td0 = stamp(dbg != nullptr);
+    if (dbg) dbg_region(dbg, kDbgDielVisits);
     float r = randf(seed);
     f3 sd;
     dielectric_scatter(dir, hn, sc->ior, r, sd);
@@ -672,7 +691,13 @@ RTP_DEV int shade_hit(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed,
     atten = mk(1.f, 1.f, 1.f);
     ps.org = hp;
     ps.dir = sd;
+    if (dbg) {
+      const unsigned long long td1 = __builtin_amdgcn_s_memtime();
+      if ((int)(threadIdx.x & 63) == (int)__builtin_ctzll(__ballot(true))) dbg_add(dbg, kDbgCyclesDiel, td1 - td0);
+    }
   } else {  // LambertianWorklet
+    const unsigned long long tg0 = stamp(dbg != nullptr);
+    if (dbg) dbg_region(dbg, kDbgGenVisits);
     f3 gen;
     float sph_ctm = -1.0f;  // sqrt(1 - R^2/|c-hp|^2) when the generator made it (sphere_pdf_value reuses it)
     uint32_t tw = wang(seed);  // which (PdfWorklet.h:20)
@@ -708,6 +733,7 @@ RTP_DEV int shade_hit(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed,
     const float m = is_cos ? 2.0f : 1.0f;
     const f3 gcs = de_nan(local(guvw, mk(cphi * m * rad, sphi * m * rad, z)));
     gen = is_quad ? genq : gcs;
+    const unsigned long long tg1 = stamp(dbg != nullptr);
     // applyPDFs: QuadPDFWorklet, SpherePDFWorklet (1 discarded draw)
     const float weight = 0.5f;
     float sum = 0;
@@ -734,6 +760,13 @@ RTP_DEV int shade_hit(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed,
     atten = mk((float)(alb.x * sctr), (float)(alb.y * sctr), (float)(alb.z * sctr));
     ps.org = hp;
     ps.dir = gen;
+    if (dbg) {  // (wave cycles: added once, by the first active lane)
+      const unsigned long long tg2 = __builtin_amdgcn_s_memtime();
+      if ((int)(threadIdx.x & 63) == (int)__builtin_ctzll(__ballot(true))) {
+        dbg_add(dbg, kDbgCyclesGen, tg1 - tg0);
+        dbg_add(dbg, kDbgCyclesPdf, tg2 - tg1);
+      }
+    }
   }
   if (d <= D - 2) {
     *hist_d = make_float4(atten.x, atten.y, atten.z, 0.f);
@@ -1028,6 +1061,7 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
   // (compiled in only for the kStats instantiation: the counters cost ~30 VGPRs)
   unsigned long long dbg[kStats ? kDbgCounters : 1] = {};
   constexpr bool want_dbg = kStats;
+  unsigned long long* const gdbg = want_dbg ? p.dbg + (int64_t)w * kDbgCounters : nullptr;
   const unsigned long long t_start = want_dbg ? __builtin_amdgcn_s_memtime() : 0ull;
   if (p.dbg && lane == 0) {  // placement + start time (RTP_DEBUG_STATS=1|2)
     p.dbg[(int64_t)w * kDbgCounters + kDbgRealStart] = __builtin_amdgcn_s_memrealtime();
@@ -1102,6 +1136,10 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
         f3 c;
         if (flags & kEndLight) {
           const int k_end = D - frem;  // a light hit ends the path: rem = D - 1 - k_end + 1
+          if (want_dbg) {
+            dbg_region(gdbg, kDbgFfRadVisits);
+            dbg_add(gdbg, kDbgFfRadRows, (unsigned long long)(k_end + 1));
+          }
           const float4* __restrict__ hp = hist_base + fslot;
           // rows k_end (E) and k_end-1 .. k_end-5 issued together (clamped to
           // row 0; rows below 0 are not applied), the rest two per trip;
@@ -1172,6 +1210,10 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
         const bool act = mine && i < frem;
         if (!__any(act)) break;
         if (act) fseed = dead_step(fseed, t1, t2);
+        if (want_dbg) {
+          const uint64_t am = __ballot(act);
+          if (lane == 0) dbg_add(gdbg, kDbgDeadLanes, (unsigned long long)__popcll(am));
+        }
         iters++;
       }
       bool again = false;
@@ -1243,6 +1285,7 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
     if (!has_path) {
       const int r = (int)lane_rank(idle);
       if (r < take) {
+        if (want_dbg) dbg_region(gdbg, kDbgRefillVisits);
         slot = q_ready[(ready_head + r) & (kPool - 1)];
         seed = s_seed[slot];
         hist = hist_base + slot;
@@ -1307,13 +1350,14 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
         wni = -1;
       } else {
         res = bounce<kBvh, true, kLdsBvh>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D,
-                                          want_dbg ? dbg : nullptr, s_qshade, s_bvh);
+                                          want_dbg ? dbg : nullptr, s_qshade, s_bvh, gdbg);
       }
       tbnc = stamp(want_dbg);
       if (res == kAlive && ps.d < D - 1) {
         ps.d++;
       } else {
         const int k_end = ps.d;
+        if (want_dbg) dbg_region(gdbg, kDbgEndVisits);
         // the radiance product runs in the fast-forward batch (above)
         if (res == kLight) hist[(int64_t)k_end * stride] = make_float4(emit.x, emit.y, emit.z, 0.f);
         // dead depths left: D-1-k_end, plus depth k_end's own draws when the
@@ -1386,7 +1430,7 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
     dbg[kDbgCyclesTotal] = __builtin_amdgcn_s_memtime() - t_start;
     dbg[kDbgRealEnd] = __builtin_amdgcn_s_memrealtime();
     dbg[kDbgTailCycles] = t_tail ? __builtin_amdgcn_s_memtime() - t_tail : 0;
-    for (int c = 0; c < (kStats ? kDbgCounters : 0); c++)
+    for (int c = 0; c < (kStats ? kDbgRefillVisits : 0); c++)  // (the later counters are accumulated in place)
       if (c != kDbgRealStart && c != kDbgHwId) p.dbg[(int64_t)w * kDbgCounters + c] = dbg[c];
   }
   wave_sync();

@@ -307,6 +307,27 @@ enum DbgCounter {
   kDbgTailCycles,        // s_memtime cycles from the first such step to the wave's end
   kDbgFallbackSteps,     // bounce steps in which some lane ran the exact scan of the prefiltered quads
   kDbgFallbackLanes,     // lanes that did, summed over all bounce steps
+  // exec occupancy per region (round 4): how often a region ran in a wave
+  // (visits) and the lanes active when it started (sum of popcount(exec))
+  kDbgRefillVisits,      // refill with >= 1 lane taking a sample: camera ray
+  kDbgRefillLanes,
+  kDbgHitVisits,         // shade_hit past the miss test (a surface was hit)
+  kDbgHitLanes,
+  kDbgGenVisits,         // the Lambertian branch: generator + pdfs + mixture
+  kDbgGenLanes,
+  kDbgCyclesGen,         //   s_memtime cycles in the generator (which draw .. gen)
+  kDbgCyclesPdf,         //   ... in the pdfs, the mixture and the scatter (gen .. atten)
+  kDbgEndVisits,         // path-end bookkeeping (a lane's path ended this step)
+  kDbgEndLanes,
+  kDbgFfRadVisits,       // fast-forward batch: the radiance product (light-hit samples)
+  kDbgFfRadLanes,
+  kDbgFfRadRows,         //   history rows read, summed over lanes
+  kDbgDeadLanes,         // hashed dead depths after the tables: active lanes summed over trips
+  kDbgDielVisits,        // the dielectric branch (glass hits)
+  kDbgDielLanes,
+  kDbgCyclesDiel,        //   s_memtime cycles in it
+  kDbgLightVisits,       // light hits (the path ends with an emission)
+  kDbgLightLanes,
   kDbgCounters
 };
 

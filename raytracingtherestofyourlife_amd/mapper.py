@@ -358,7 +358,10 @@ class Device:
     DEBUG_COUNTERS = ("bounce_steps", "bounce_lanes", "ff_phases", "ff_lanes", "ff_iters", "cycles_bounce",
                       "cycles_ff", "cycles_total", "cycles_intersect", "cycles_bounce_call", "cycles_end",
                       "cycles_refill", "real_start", "real_end", "hw_id", "tail_steps", "tail_lanes",
-                      "tail_cycles", "fallback_steps", "fallback_lanes", "max_wave_cycles")
+                      "tail_cycles", "fallback_steps", "fallback_lanes", "refill_visits", "refill_lanes",
+                      "hit_visits", "hit_lanes", "gen_visits", "gen_lanes", "cycles_gen", "cycles_pdf", "end_visits",
+                      "end_lanes", "ffrad_visits", "ffrad_lanes", "ffrad_rows", "dead_lanes", "diel_visits", "diel_lanes",
+                      "cycles_diel", "light_visits", "light_lanes", "max_wave_cycles")
 
     def debug_counters(self) -> dict:
         """Pool-kernel counters of the last launch made with RTP_DEBUG_STATS=1."""

@@ -43,6 +43,18 @@ c.update(kernel_ms=st.kernel_ms, samples=samples, live_bounces=L,
          tail_frac_cycles=c["tail_cycles"] / max(1, c["cycles_total"]),
          fallback_frac_steps=c["fallback_steps"] / max(1, c["bounce_steps"]),
          fallback_lanes_per_step=c["fallback_lanes"] / max(1, c["bounce_steps"]))
+# exec occupancy per region (round 4): lanes active at the region's start
+regions = {"bounce (intersect)": ("bounce_steps", "bounce_lanes"), "surface hit (shade)": ("hit_visits", "hit_lanes"),
+           "Lambertian (generator + pdfs)": ("gen_visits", "gen_lanes"), "dielectric": ("diel_visits", "diel_lanes"),
+           "light hit": ("light_visits", "light_lanes"), "path end": ("end_visits", "end_lanes"),
+           "refill (camera ray)": ("refill_visits", "refill_lanes"), "fast-forward batch": ("ff_phases", "ff_lanes"),
+           "  radiance product": ("ffrad_visits", "ffrad_lanes"), "  hashed dead depths": ("ff_iters", "dead_lanes")}
+c["regions"] = {k: {"visits": c[v], "visits_per_step": round(c[v] / max(1, c["bounce_steps"]), 4),
+                    "lanes": round(c[l] / max(1, c[v]), 2)} for k, (v, l) in regions.items()}
+c["regions"]["  radiance product"]["rows_per_lane"] = round(c["ffrad_rows"] / max(1, c["ffrad_lanes"]), 2)
+c["per_step_gen"] = c["cycles_gen"] / max(1, c["bounce_steps"])
+c["per_step_pdf"] = c["cycles_pdf"] / max(1, c["bounce_steps"])
+c["per_step_diel"] = c["cycles_diel"] / max(1, c["bounce_steps"])
 print(json.dumps(c, indent=1))
 rec = dev.debug_wave_records()
 import numpy as np

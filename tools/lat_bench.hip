@@ -1,0 +1,174 @@
+// lat_bench.hip -- latency and throughput of the bounce step's parts on one
+// MI355X, outside the pool kernel's scheduling (development tool).
+//
+// Each lane runs a chain of bounces in the C2 scene (Cornell box, variant 0):
+// a random ray from a random point inside the room, then from each hit point
+// on: closest_hit (+ shade_hit: material, generator, pdfs, scatter) exactly as
+// the render kernel runs them (the device functions of rtp_kernels.hip,
+// included below).  A path that dies restarts from a random point.  W waves
+// per SIMD (grid = CUs x W blocks of 4 waves): W = 1 gives a lone wave's
+// latency per step, W = 5 the pool kernel's occupancy.
+//
+// modes: 0 closest_hit only (prefilter on)
+//        1 closest_hit + shade_hit (a bounce step without the pool's bookkeeping)
+//        2 closest_hit with the prefilter off (exact scan of every quad)
+//        3 shade_hit only (the hit of the first ray, re-shaded each step)
+//        4 one jump-table gather per step (HBM latency: a dependent 4-byte
+//          gather from a 16 GiB table, the fast-forward's chain read)
+//
+// build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off -fno-fast-math
+//        -I raytracingtherestofyourlife_amd/csrc tools/lat_bench.hip
+//        -L raytracingtherestofyourlife_amd -lrtp -Wl,-rpath,<that dir> -o tools/lat_bench
+// usage: tools/lat_bench [iters] [modes...]
+#include "../raytracingtherestofyourlife_amd/csrc/rtp_kernels.hip"
+#include "../raytracingtherestofyourlife_amd/csrc/rtp_context.hpp"
+
+#include <vector>
+
+namespace lb {
+using namespace rtp;
+
+RTP_DEV f3 rand_dir(uint32_t& s) {
+  for (;;) {
+    const float x = 2.f * randf(s) - 1.f, y = 2.f * randf(s) - 1.f, z = 2.f * randf(s) - 1.f;
+    const float q = x * x + y * y + z * z;
+    if (q > 1e-4f && q <= 1.f) return mk(x, y, z);
+  }
+}
+RTP_DEV f3 rand_point(uint32_t& s) {
+  return mk(0.05f + 0.9f * randf(s), 0.05f + 0.9f * randf(s), 0.05f + 0.9f * randf(s));
+}
+
+template <int kMode>
+__global__ void __launch_bounds__(256) lat_kernel(const DevScene* __restrict__ sc, int iters, float4* hist,
+                                                  const uint32_t* __restrict__ tab, unsigned long long* cycles,
+                                                  float* sink) {
+  __shared__ __align__(16) float s_qshade[kQTableFloats];
+  fill_qshade(sc, s_qshade);
+  __syncthreads();
+  const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  uint32_t seed = 0x9e3779b9u * (blockIdx.x * blockDim.x + threadIdx.x + 1);
+  Path ps;
+  ps.org = rand_point(seed);
+  ps.dir = rand_dir(seed);
+  ps.d = 0;
+  ps.nonfinite = false;
+  float acc = 0.f;
+  float4* hd = hist + blockIdx.x * blockDim.x + threadIdx.x;
+  Hit h0{};
+  Path p0 = ps;
+  if (kMode == 3) h0 = closest_hit<false>(sc, ps.org, ps.dir, true, nullptr, s_qshade + kPrexLdsOffset);
+  uint32_t ts = seed;
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < iters; i++) {
+    if constexpr (kMode == 4) {
+      ts = tab[ts];
+      acc += (float)(ts & 1u);
+    } else if constexpr (kMode == 3) {
+      ps = p0;
+      f3 emit;
+      const int r = shade_hit<false, true>(sc, ps, seed, emit, hd, 50, s_qshade, h0);
+      acc += ps.dir.x + (float)r;
+    } else {
+      const Hit h = closest_hit<false>(sc, ps.org, ps.dir, kMode != 2, nullptr, s_qshade + kPrexLdsOffset);
+      if constexpr (kMode == 0 || kMode == 2) {
+        acc += h.t;
+        ps.org = h.kind >= 0 ? add(ps.org, scl(ps.dir, h.t)) : rand_point(seed);
+        ps.dir = rand_dir(seed);
+      } else {
+        f3 emit;
+        const int r = shade_hit<false, true>(sc, ps, seed, emit, hd, 50, s_qshade, h);
+        if (r != kAlive) {
+          acc += emit.x;
+          ps.org = rand_point(seed);
+          ps.dir = rand_dir(seed);
+        }
+      }
+    }
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  if ((threadIdx.x & 63) == 0) cycles[gw] = t1 - t0;
+  sink[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
+__global__ void fill_tab(uint32_t* t, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    uint32_t x = (uint32_t)i * 2654435761u;
+    x ^= x >> 15;
+    t[i] = x * 2246822519u;
+  }
+}
+
+template <int kMode>
+void run(const DevScene* sc, int cus, int w, int iters, float4* hist, const uint32_t* tab, unsigned long long* cyc,
+         float* sink) {
+  const int blocks = cus * w;
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  hipLaunchKernelGGL(lat_kernel<kMode>, dim3(blocks), dim3(256), 0, nullptr, sc, 4, hist, tab, cyc, sink);  // warm
+  (void)hipEventRecord(a, nullptr);
+  hipLaunchKernelGGL(lat_kernel<kMode>, dim3(blocks), dim3(256), 0, nullptr, sc, iters, hist, tab, cyc, sink);
+  (void)hipEventRecord(b, nullptr);
+  (void)hipEventSynchronize(b);
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, a, b);
+  std::vector<unsigned long long> c((size_t)blocks * 4);
+  (void)hipMemcpy(c.data(), cyc, c.size() * 8, hipMemcpyDeviceToHost);
+  double sum = 0, mx = 0;
+  for (auto v : c) sum += (double)v, mx = std::max(mx, (double)v);
+  printf("{\"mode\": %d, \"waves_per_simd\": %d, \"iters\": %d, \"kernel_ms\": %.3f, \"cycles_per_step\": %.1f, "
+         "\"max_cycles_per_step\": %.1f, \"ns_per_step_wall\": %.2f, \"wave_steps_per_us\": %.1f}\n",
+         kMode, w, iters, ms, sum / c.size() / iters, mx / iters, ms * 1e6 / iters, (double)c.size() * iters / (ms * 1e3));
+  fflush(stdout);
+}
+}  // namespace lb
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? atoi(argv[1]) : 2000;
+  std::vector<int> modes;
+  for (int i = 2; i < argc; i++) modes.push_back(atoi(argv[i]));
+  if (modes.empty()) modes = {0, 1, 2, 3, 4};
+  rtp_context* ctx = nullptr;
+  if (rtp_create(0, &ctx) != RTP_OK) {
+    fprintf(stderr, "rtp_create: %s\n", rtp_last_error());
+    return 1;
+  }
+  rtp_scene_desc d{};
+  if (rtp_cornell_box(0, &d) != RTP_OK || rtp_set_scene(ctx, &d) != RTP_OK) {
+    fprintf(stderr, "scene: %s\n", rtp_last_error());
+    return 1;
+  }
+  int cus = 0;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+  const int maxw = 5;
+  float4* hist = nullptr;
+  uint32_t* tab = nullptr;
+  unsigned long long* cyc = nullptr;
+  float* sink = nullptr;
+  (void)hipMalloc(&hist, (size_t)cus * maxw * 256 * 16 * 64);
+  (void)hipMalloc(&cyc, (size_t)cus * maxw * 4 * 8);
+  (void)hipMalloc(&sink, (size_t)cus * maxw * 256 * 4);
+  const size_t tab_n = (size_t)1 << 32;
+  bool have_tab = false;
+  for (int m : modes) have_tab |= m == 4;
+  if (have_tab) {  // a scrambled map: the gather chain is data-dependent and spans the whole table
+    if (hipMalloc(&tab, tab_n * 4) != hipSuccess) return 1;
+    hipLaunchKernelGGL(lb::fill_tab, dim3((unsigned)(tab_n / 256)), dim3(256), 0, nullptr, tab, (uint64_t)tab_n);
+    (void)hipDeviceSynchronize();
+  }
+  for (int m : modes)
+    for (int w = 1; w <= maxw; w++) {
+      switch (m) {
+        case 0: lb::run<0>(ctx->d_scene, cus, w, iters, hist, tab, cyc, sink); break;
+        case 1: lb::run<1>(ctx->d_scene, cus, w, iters, hist, tab, cyc, sink); break;
+        case 2: lb::run<2>(ctx->d_scene, cus, w, iters, hist, tab, cyc, sink); break;
+        case 3: lb::run<3>(ctx->d_scene, cus, w, iters, hist, tab, cyc, sink); break;
+        case 4: lb::run<4>(ctx->d_scene, cus, w, iters, hist, tab, cyc, sink); break;
+        default: break;
+      }
+    }
+  rtp_destroy(ctx);
+  return 0;
+}
