@@ -66,6 +66,18 @@ RTP_DEV float sqrt_fast(float x) {  // v_sqrt_f32 + residual-based rounding fix 
   return s;
 }
 
+// RN(a / b) from r = RN(1 / b): q = RN(a r) is within one ulp of a / b, the
+// remainder a - b q is exact with an FMA, and one FMA correction rounds to
+// the correctly rounded quotient (Markstein's theorem; Muller et al.,
+// Handbook of Floating-Point Arithmetic, 2nd ed., Thm 5.8), provided nothing
+// over- or underflows.  Callers document why their operands stay in range;
+// rtp_verify_fast_math kind 8 checks it exhaustively over divisors.
+RTP_DEV float div_markstein(float a, float b, float r) {
+  const float q = a * r;
+  const float rem = __builtin_fmaf(-b, q, a);
+  return __builtin_fmaf(rem, r, q);
+}
+
 // ------------------------------------------------------ exact wrappers ---
 // rcp_nr1(x) == 1.0f/x and sqrt_fast(x) == sqrtf(x) bit for bit for every
 // float with |x| in [2^-40, 2^40] (exhaustive device check, tools/
@@ -105,12 +117,17 @@ RTP_DEV float rsqrt_exact(float x) {  // 1 / sqrtf(x)  (vtkm::RMagnitude, CPU bu
 // 1/det of the quad tests.  The reciprocal is only used when !(|det| < kEps)
 // (kEps = 1e-5 > 2^-40), so the small end of fast_range never matters: only
 // |det| > 2^40 (or NaN) takes the IEEE path.
+#ifndef RTP_DET_FALLBACK
+#define RTP_DET_FALLBACK 1  // (0: timing experiments only -- not exact for |det| > 2^40)
+#endif
 RTP_DEV float rcp_det(float x) {
   float r = rcp_nr1(x);
-  const bool slow = !(fabsf(x) <= 0x1p40f);
-  if (__ballot(slow)) {
-    asm volatile("");
-    if (slow) r = 1.0f / x;
+  if (RTP_DET_FALLBACK) {
+    const bool slow = !(fabsf(x) <= 0x1p40f);
+    if (__ballot(slow)) {
+      asm volatile("");
+      if (slow) r = 1.0f / x;
+    }
   }
   return r;
 }
@@ -475,17 +492,34 @@ RTP_DEV float sphere_pdf_value(const DevLights& L, f3 o, f3 v, float ctm = -1.0f
 }
 
 // DielectricWorklet (EmitWorklet.h:153-226)
-// pow(x, 5.0) in double.  Inlined, the compiler hoists its ~15 double
-// polynomial constants out of the render loop into ~30 VGPRs held for the
-// whole kernel (and spills around them); as a call they live only in the
-// callee, which runs on dielectric hits alone.
-__device__ __attribute__((noinline)) double pow5(double x) { return pow(x, 5.0); }
-RTP_DEV float schlick(float cosine, float ref_idx) {
-  float r0 = (1 - ref_idx) / (1 + ref_idx);
-  r0 = r0 * r0;
-  return (float)(r0 + (1 - r0) * pow5((double)(1 - cosine)));
+// pow((double)(1 - cosine), 5.0) of schlick: x is a float value (24
+// significant bits), so x^2 is exact in double and x^4 = h + l exactly (the
+// error of a product is a double, recovered by an FMA); x^5 = (h + l) x =
+// p + e + l x with p + e = h x exact.  The sum rounds once more: the result
+// is the correctly rounded x^5 unless x^5 lies within ~2^-100 (relative) of a
+// midpoint between doubles.  glibc's pow (the reference's; the oracle's) is
+// correctly rounded but for such near-midpoint cases too, and the value
+// reaches the image only through (float)(r0 + (1 - r0) x^5) and a comparison
+// with a float draw.  Checked against this host's glibc pow for every float
+// x with |x| in [2^-24, 2] (tests/cpp/pow5_check.cpp).  The ocml pow it
+// replaces ran ~80 double operations in a call on 7 of 64 lanes in 94% of
+// C2's bounce steps (r04c stats: 9% of the step).  Range: |1 - cosine| is 0
+// or >= 2^-24 and <= 2.5, so nothing under- or overflows; NaN propagates.
+RTP_DEV double pow5_exact(double x) {
+  const double x2 = x * x;                      // exact
+  const double h = x2 * x2;                     // x^4 rounded
+  const double l = __builtin_fma(x2, x2, -h);   // ... and its exact error
+  const double p = h * x;
+  const double e = __builtin_fma(h, x, -p);     // h x = p + e exactly
+  return p + (e + l * x);
 }
-RTP_DEV void dielectric_scatter(f3 dir, f3 n, float ref_idx, float rnd, f3& sd) {
+// r0sq = ((1 - ref_idx) / (1 + ref_idx))^2 (precomputed on the host with the
+// same float operations: DevScene::ior_r0sq)
+RTP_DEV float schlick(float cosine, float r0sq) {
+  return (float)(r0sq + (1 - r0sq) * pow5_exact((double)(1 - cosine)));
+}
+// ior_inv = (float)(1.0 / ref_idx) (DevScene::ior_inv)
+RTP_DEV void dielectric_scatter(f3 dir, f3 n, float ref_idx, float r0sq, float ior_inv, float rnd, f3& sd) {
   f3 reflected = sub(dir, scl(n, 2 * dot(dir, n)));
   f3 refracted = mk(0, 0, 0);  // reference reads an uninitialised vec3 here when refraction fails and rnd==1
   f3 outward;
@@ -497,7 +531,7 @@ RTP_DEV void dielectric_scatter(f3 dir, f3 n, float ref_idx, float rnd, f3& sd) 
     cosine = ref_idx * dot(dir, n) * rm;
   } else {
     outward = n;
-    ni_over_nt = (float)(1.0 / ref_idx);
+    ni_over_nt = ior_inv;
     cosine = -dot(dir, n) * rm;
   }
   float reflect_prob;
@@ -507,7 +541,7 @@ RTP_DEV void dielectric_scatter(f3 dir, f3 n, float ref_idx, float rnd, f3& sd) 
     float discriminant = (float)(1.0 - ni_over_nt * ni_over_nt * (1 - dt * dt));
     if (discriminant > 0) {
       refracted = sub(scl(sub(uv, scl(outward, dt)), ni_over_nt), scl(outward, sqrt_exact(discriminant)));
-      reflect_prob = schlick(cosine, ref_idx);
+      reflect_prob = schlick(cosine, r0sq);
     } else {
       reflect_prob = 1.0f;
     }

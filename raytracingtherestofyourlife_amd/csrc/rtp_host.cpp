@@ -22,7 +22,7 @@
 #include "rtp_context.hpp"
 #include "rtp_layout.hpp"
 
-extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int bvh, int* variant_out, int* waves_out);
+extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int spp, int bvh, int* variant_out, int* waves_out);
 extern "C" int rtp_plan_steal(int64_t npix, int bvh);
 extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::KParams* p, int variant, int waves, int bvh,
                                         hipStream_t stream, int n_lnodes);
@@ -865,6 +865,11 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
   h->light.sr = s->sphere_radius[0];  // SphereRadii[0] (PdfWorklet.h:205-210)
   h->light.srr = h->light.sr * h->light.sr;
   h->ior = s->ior;
+  {  // schlick's r0^2 and 1/ior with the reference's operations (float, float; double then float)
+    float r0 = (1 - h->ior) / (1 + h->ior);
+    h->ior_r0sq = r0 * r0;
+    h->ior_inv = (float)(1.0 / h->ior);
+  }
   h->which_t1 = which_threshold(2);
   h->which_t2 = which_threshold(3);
   hipError_t e = hipSetDevice(c->device);
@@ -1019,7 +1024,7 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
   const char* stats_env = getenv("RTP_DEBUG_STATS");
   const bool stats_on = stats_env && stats_env[0] == '1';
   const int bvh = !c->use_bvh ? 0 : (c->n_lnodes > 0 && !stats_on && !d_wave_begin) ? 2 : 1;
-  int64_t lanes = rtp_plan_history_lanes(npix, bvh, &variant, &waves);
+  int64_t lanes = rtp_plan_history_lanes(npix, spp, bvh, &variant, &waves);
   if (d_wave_begin) {  // a planned launch: the caller's waves
     if (variant != 2 || c->use_bvh || tile)
       return fail(RTP_ERR_INVALID_ARGUMENT, "render: a wave plan needs the pool kernel, no BVH, no tile deal");
@@ -1322,7 +1327,7 @@ rtp_status rtp_debug_closest_hit(rtp_context* c, const float* rays, int64_t n, u
 // see rtp_verify_fast_math_kernel) over float bit patterns [lo_bits, hi_bits].
 rtp_status rtp_verify_fast_math(rtp_context* c, int32_t kind, uint32_t lo_bits, uint32_t hi_bits,
                                 uint64_t* mismatches, uint32_t* first_bad) {
-  if (!c || !mismatches || hi_bits < lo_bits || kind < 0 || kind > 7)
+  if (!c || !mismatches || hi_bits < lo_bits || kind < 0 || kind > 8)
     return fail(RTP_ERR_INVALID_ARGUMENT, "rtp_verify_fast_math: bad args");
   HIP_TRY(hipSetDevice(c->device));
   unsigned long long* d_bad = nullptr;

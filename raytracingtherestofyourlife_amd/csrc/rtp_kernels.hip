@@ -578,7 +578,14 @@ RTP_DEV f3 camera_ray(const Cam& cam, int pi, int pj, int nx, int ny, uint32_t& 
   if (rd.y == 0.f) rd.y += 0.0000001f;
   if (rd.z == 0.f) rd.z += 0.0000001f;
   float sq_mag = __builtin_sqrtf(dot(rd, rd));
-  return mk(rd.x / sq_mag, rd.y / sq_mag, rd.z / sq_mag);
+  // rd.x / sq_mag, ... as Markstein divisions by one reciprocal: rd =
+  // nlook + a*dx + b*dy with dx, dy orthogonal to the unit nlook (Camera.cxx:
+  // 437-474), so sq_mag is >= ~1 and at most ~|tan(fov/2)| + 1 < 2^26 for fov
+  // <= 180: inside rcp_nr1's exact range [2^-40, 2^40]; each |component| is
+  // <= sq_mag and >= 1e-7 (the zero fix above), so no quotient or remainder
+  // under- or overflows.
+  const float r = rcp_nr1(sq_mag);
+  return mk(div_markstein(rd.x, sq_mag, r), div_markstein(rd.y, sq_mag, r), div_markstein(rd.z, sq_mag, r));
 }
 
 struct Path {
@@ -685,7 +692,7 @@ RTP_DEV int shade_hit(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed,
     if (dbg) dbg_region(dbg, kDbgDielVisits);
     float r = randf(seed);
     f3 sd;
-    dielectric_scatter(dir, hn, sc->ior, r, sd);
+    dielectric_scatter(dir, hn, sc->ior, sc->ior_r0sq, sc->ior_inv, r, sd);
     seed = dead_step(seed, t1, t2);  // generation draws (direction unused)
     (void)randf(seed);               // SpherePDFWorklet's discarded draw
     atten = mk(1.f, 1.f, 1.f);
@@ -1557,6 +1564,21 @@ __global__ void rtp_verify_fast_math_kernel(int kind, uint32_t lo, uint64_t coun
     case 5: want = (float)((double)x / kPi); got = cos_over_pi(x); break;
     case 6: { float s, c; rtp_sincosf(x, &s, &c); want = rtp_sinf(x); got = s; break; }
     case 7: { float s, c; rtp_sincosf(x, &s, &c); want = rtp_cosf(x); got = c; break; }
+    case 8: {  // x as the divisor of div_markstein, 32 numerators spread over [-x, x] and beyond
+      const float r = rcp_nr1(x);
+      uint32_t h = bits;
+      for (int k = 0; k < 32; k++) {
+        h = wang(h + (uint32_t)k);
+        const float a = x * ((float)(int32_t)h * 0x1p-31f) * (k < 24 ? 1.0f : 1024.0f);
+        const float w = a / x, g = div_markstein(a, x, r);
+        if (__float_as_uint(w) != __float_as_uint(g) && fabsf(w) >= 0x1p-120f) {  // (normal quotients)
+          want = w;
+          got = g;
+          break;
+        }
+      }
+      break;
+    }
     default: break;
   }
   if (__float_as_uint(want) != __float_as_uint(got)) {
@@ -1633,7 +1655,7 @@ int kernel_variant() {
 }  // namespace
 
 // Work plan: how many lanes' worth of attenuation history the launch needs.
-extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int bvh, int* variant_out, int* waves_out) {
+extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int spp, int bvh, int* variant_out, int* waves_out) {
   const int v = kernel_variant();
   if (variant_out) *variant_out = v;
   if (v == 1) {
@@ -1655,9 +1677,19 @@ extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int bvh, int* variant_ou
   // and a second pixel on a lane only lengthens its chain (C1: 0.70 -> 0.80
   // ms at 80), so such launches keep 64.  RTP_WAVE_PIXELS overrides
   // (experiments).
+  // Long chains (spp >= 2048) on a share that fills 1.5-2.5 waves per SIMD
+  // at 128 pixels per wave take 128: every pixel's chain is then ~2x the
+  // average sample chain of a lane's two pixels, so the lanes stay full, and
+  // fewer waves per SIMD make each step of the longest chains faster (the
+  // per-step cost rises ~2.5 k cycles per extra wave on a SIMD, 13 k alone:
+  // tools/lat_bench.hip).  C4's 1/8 share (259 200 pixels, 4096 spp), kernel
+  // ms (r04c): 80 px/wave 388, 96 323, 112 354, 128 310.  C2's shares keep
+  // 64/80 (1000 spp: 128 px/wave was 9-10% slower at N = 2, 4, 8).
   const char* st = getenv("RTP_DEBUG_STATS");
   const int64_t resident = pool_resident_waves(st && st[0] == '1', bvh);
+  const int64_t simds = std::max<int64_t>(1, resident / RTP_POOL_MIN_WAVES_PER_EU);
   int wave_px = (npix + 63) / 64 * 3 < resident ? 64 : 80;
+  if (spp >= 2048 && npix * 2 >= simds * 128 * 3 && npix * 2 <= simds * 128 * 5) wave_px = 128;
   if (const char* e = getenv("RTP_WAVE_PIXELS")) wave_px = std::max(1, std::min(rtp::kPool, atoi(e)));
   const int64_t by_lanes = (npix + wave_px - 1) / wave_px;
   const int64_t by_pool = (npix + rtp::kPool - 1) / rtp::kPool;

@@ -191,7 +191,10 @@ struct alignas(16) DevScene {
   float ior;
   int32_t n_nodes;                 // BVH scenes (n_spheres >= kBvhMinSpheres): nodes per octant copy
   int32_t n_lnodes;                // LDS walk: nodes of lnodes (0: none)
-  int32_t pad[2];
+  // DielectricWorklet constants of ior, with the reference's float/double
+  // operations (EmitWorklet.h:153-170): r0 = ((1 - ior) / (1 + ior))^2 of
+  // schlick, and ni_over_nt = (float)(1.0 / ior) of a ray entering the glass
+  float ior_r0sq, ior_inv;
   const BvhNode* nodes;            // 8 * n_nodes: one threaded copy per ray-direction octant
   const DevSphereG* sph_geom;      // BVH leaf order
   const DevSphere* sph_all;        // scene order (materials of the hit sphere)

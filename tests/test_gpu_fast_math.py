@@ -37,3 +37,13 @@ def test_branch_free_sincos_equals_ports(device, kind, name):
     every float in [0, 2pi] (phi = float(2*pi*r), r in [0, 1])."""
     bad, first = device.verify_fast_math(kind, 0.0, 6.2831855)
     assert bad == 0, f"sincos/{name}: {bad} mismatches, first bit pattern {first:#x}"
+
+
+def test_markstein_division_exact(device):
+    """div_markstein(a, b, rcp_nr1(b)) == a / b (IEEE) for EVERY float divisor b
+    with |b| in [2^-20, 2^26] (camera_ray's |rd|: >= ~1, < 2^26) and 32
+    numerators per divisor spread over [-b, b] and [-1024 b, 1024 b]
+    (rtp_verify_fast_math kind 8; normal quotients)."""
+    for lo, hi in ((2.0**-20, 2.0**26), (-(2.0**-20), -(2.0**26))):
+        bad, first = device.verify_fast_math(8, lo, hi)
+        assert bad == 0, f"markstein: {bad} mismatches, first divisor bit pattern {first:#x}"

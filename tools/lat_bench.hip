@@ -15,6 +15,10 @@
 //        3 shade_hit only (the hit of the first ray, re-shaded each step)
 //        4 one jump-table gather per step (HBM latency: a dependent 4-byte
 //          gather from a 16 GiB table, the fast-forward's chain read)
+//        5 the ray advance alone (random point / direction: the other modes' overhead)
+//        6 closest_hit's always-exact scan alone (kinds 7..10, 0)
+//        7 closest_hit's prefilter alone (axis-plane quads + the candidate's exact test)
+// (built with -DRTP_DET_FALLBACK=0: the quad tests without their |det| > 2^40 branch)
 //
 // build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off -fno-fast-math
 //        -I raytracingtherestofyourlife_amd/csrc tools/lat_bench.hip
@@ -37,6 +41,45 @@ RTP_DEV f3 rand_dir(uint32_t& s) {
 }
 RTP_DEV f3 rand_point(uint32_t& s) {
   return mk(0.05f + 0.9f * randf(s), 0.05f + 0.9f * randf(s), 0.05f + 0.9f * randf(s));
+}
+
+// the two parts of closest_hit (rtp_kernels.hip), each alone
+template <int kPart>
+RTP_DEV uint64_t ch_part(const DevScene* __restrict__ sc, f3 o, f3 d, const float* lds_prex) {
+  uint64_t key = kNoHitKey;
+  if constexpr (kPart == 0) {
+    const int g6 = sc->kind_begin[6], g7 = sc->kind_begin[7], g8 = sc->kind_begin[8], g9 = sc->kind_begin[9],
+              g10 = sc->kind_begin[10], g11 = sc->kind_begin[11];
+    u16v cur = quad_head(sc, g6);
+    scan_kind_pf<7>(sc, g6, g7, o, d, key, cur);
+    scan_kind_pf<8>(sc, g7, g8, o, d, key, cur);
+    scan_kind_pf<9>(sc, g8, g9, o, d, key, cur);
+    scan_kind_pf<10>(sc, g9, g10, o, d, key, cur);
+    scan_kind_pf<0>(sc, g10, g11, o, d, key, cur);
+  } else {
+    const float dmax = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fmaxf(fabsf(d.z), 1.0f));
+    const float omax = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+    const float ma = kPreK * dmax, mb = kPreK * (omax + (sc->pre_scale + 1.0f));
+    uint32_t k1 = ~0u, k2 = ~0u;
+    const int p0 = sc->pre_begin[0], p1 = sc->pre_begin[1], p2 = sc->pre_begin[2], p3 = sc->pre_begin[3];
+    u8v pcur = pre_rec(sc, p0);
+    pre_axis<0>(sc, p0, p1, o, d, ma, mb, k1, k2, pcur);
+    pre_axis<1>(sc, p1, p2, o, d, ma, mb, k1, k2, pcur);
+    pre_axis<2>(sc, p2, p3, o, d, ma, mb, k1, k2, pcur);
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v* lx = reinterpret_cast<const f4v*>(lds_prex) + 4 * (k1 & 31u);
+    f4v xr[4] = {lx[0], lx[1], lx[2], lx[3]};
+    if (k1 != ~0u) {
+      PreExact Q;
+      __builtin_memcpy(&Q, xr, sizeof(Q));
+      float t;
+      const bool ok = quad_hit_axis(Q, o, d, t);
+      const uint64_t kq = (uint64_t)__float_as_uint(t) << 32 | Q.key_lo;
+      key = (ok && t > 0.001f && kq < key) ? kq : key;
+    }
+    key ^= (uint64_t)k2;
+  }
+  return key;
 }
 
 template <int kMode>
@@ -64,6 +107,15 @@ __global__ void __launch_bounds__(256) lat_kernel(const DevScene* __restrict__ s
     if constexpr (kMode == 4) {
       ts = tab[ts];
       acc += (float)(ts & 1u);
+    } else if constexpr (kMode == 5) {
+      acc += ps.dir.x;
+      ps.org = add(ps.org, scl(ps.dir, 1e-3f * randf(seed)));
+      ps.dir = rand_dir(seed);
+    } else if constexpr (kMode == 6 || kMode == 7) {
+      const uint64_t k = ch_part<kMode - 6>(sc, ps.org, ps.dir, s_qshade + kPrexLdsOffset);
+      acc += __uint_as_float((uint32_t)(k >> 32) & 0x3fffffffu);
+      ps.org = add(ps.org, scl(ps.dir, 1e-3f * randf(seed)));
+      ps.dir = rand_dir(seed);
     } else if constexpr (kMode == 3) {
       ps = p0;
       f3 emit;
@@ -91,10 +143,10 @@ __global__ void __launch_bounds__(256) lat_kernel(const DevScene* __restrict__ s
   sink[blockIdx.x * blockDim.x + threadIdx.x] = acc;
 }
 
-__global__ void fill_tab(uint32_t* t, uint64_t n) {
+__global__ void fill_tab(uint32_t* t, uint64_t n, uint64_t base) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
-    uint32_t x = (uint32_t)i * 2654435761u;
+    uint32_t x = (uint32_t)(base + i) * 2654435761u;
     x ^= x >> 15;
     t[i] = x * 2246822519u;
   }
@@ -129,7 +181,7 @@ int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 2000;
   std::vector<int> modes;
   for (int i = 2; i < argc; i++) modes.push_back(atoi(argv[i]));
-  if (modes.empty()) modes = {0, 1, 2, 3, 4};
+  if (modes.empty()) modes = {0, 1, 2, 3, 4, 5, 6, 7};
   rtp_context* ctx = nullptr;
   if (rtp_create(0, &ctx) != RTP_OK) {
     fprintf(stderr, "rtp_create: %s\n", rtp_last_error());
@@ -155,8 +207,10 @@ int main(int argc, char** argv) {
   for (int m : modes) have_tab |= m == 4;
   if (have_tab) {  // a scrambled map: the gather chain is data-dependent and spans the whole table
     if (hipMalloc(&tab, tab_n * 4) != hipSuccess) return 1;
-    hipLaunchKernelGGL(lb::fill_tab, dim3((unsigned)(tab_n / 256)), dim3(256), 0, nullptr, tab, (uint64_t)tab_n);
-    (void)hipDeviceSynchronize();
+    for (uint64_t base = 0; base < tab_n; base += 1ull << 30)  // (a dispatch holds < 2^32 work-items)
+      hipLaunchKernelGGL(lb::fill_tab, dim3((unsigned)((1ull << 30) / 256)), dim3(256), 0, nullptr, tab + base,
+                         (uint64_t)(1ull << 30), base);
+    if (hipDeviceSynchronize() != hipSuccess) return 1;
   }
   for (int m : modes)
     for (int w = 1; w <= maxw; w++) {
@@ -166,6 +220,9 @@ int main(int argc, char** argv) {
         case 2: lb::run<2>(ctx->d_scene, cus, w, iters, hist, tab, cyc, sink); break;
         case 3: lb::run<3>(ctx->d_scene, cus, w, iters, hist, tab, cyc, sink); break;
         case 4: lb::run<4>(ctx->d_scene, cus, w, iters, hist, tab, cyc, sink); break;
+        case 5: lb::run<5>(ctx->d_scene, cus, w, iters, hist, tab, cyc, sink); break;
+        case 6: lb::run<6>(ctx->d_scene, cus, w, iters, hist, tab, cyc, sink); break;
+        case 7: lb::run<7>(ctx->d_scene, cus, w, iters, hist, tab, cyc, sink); break;
         default: break;
       }
     }
