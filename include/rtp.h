@@ -296,6 +296,14 @@ int32_t rtp_debug_counters(rtp_context* ctx, uint64_t* out, int32_t n_out);
  * bits, kind, index), 1 if the ray fell back to the exact scan. */
 rtp_status rtp_debug_closest_hit(rtp_context* ctx, const float* rays, int64_t n, uint32_t* out);
 
+/* Diagnostics: how the current scene's spheres are searched by a render
+ * (rtp_render*, without RTP_DEBUG_STATS or a wave plan): 0 every sphere in
+ * order (fewer than 9 spheres), 1 the threaded sphere BVH in global memory,
+ * 2 the same walk over each block's LDS copy of a wider-leaved tree (opt-in:
+ * RTP_BVH_LDS=1 at rtp_set_scene, and only when its nodes and spheres fit the
+ * LDS). */
+int32_t rtp_sphere_walk(rtp_context* ctx);
+
 /* Diagnostics: exhaustively compare a fast device arithmetic sequence with the
  * IEEE operation for every float bit pattern in [lo_bits, hi_bits].  kind 0:
  * rcp (v_rcp + 1 Newton step) vs 1.0f/x; 1: rcp + remainder correction; 2:

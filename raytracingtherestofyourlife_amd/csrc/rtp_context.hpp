@@ -25,8 +25,13 @@ struct rtp_context {
   int32_t* d_cidx = nullptr;     // scene index of each compact sphere leaf
   rtp::DevSphereG* d_sph_geom = nullptr;
   rtp::DevSphere* d_sph_all = nullptr;
-  rtp::LdsBvhNode* d_lnodes = nullptr;  // the LDS walk's copy of the tree (small BVH scenes)
-  int n_lnodes = 0;
+  // the LDS walk's tree (rtp_layout.hpp kLdsWalkLeaf): compact nodes, their
+  // embedded spheres' scene indices, leaf spheres (float4) and their indices
+  uint32_t* d_lw_nodes = nullptr;
+  int32_t* d_lw_cidx = nullptr;
+  float* d_lw_sph = nullptr;
+  int32_t* d_lw_orig = nullptr;
+  int lw_bytes = 0;  // its LDS footprint (0: the scene has no LDS walk)
   bool use_bvh = false;
   int ff_policy = 0;  // rtp_ff_policy (RNG jump tables)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;

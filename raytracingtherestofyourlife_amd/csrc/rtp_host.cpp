@@ -25,7 +25,8 @@
 extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int spp, int bvh, int* variant_out, int* waves_out);
 extern "C" int rtp_plan_steal(int64_t npix, int bvh);
 extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::KParams* p, int variant, int waves, int bvh,
-                                        hipStream_t stream, int n_lnodes);
+                                        hipStream_t stream, int lds_bytes);
+extern "C" int rtp_lds_walk_capacity(void);
 extern "C" hipError_t rtp_launch_eval_primitive(int kind, const void* in, void* out, int64_t n, const uint32_t* tab,
                                                 uint32_t t1, uint32_t t2, hipStream_t stream);
 extern "C" hipError_t rtp_launch_build_ff_tables(const rtp::FfBuildOut* out, int max_r, uint32_t t1, uint32_t t2,
@@ -398,7 +399,8 @@ float half_area(const float lo[3], const float hi[3]) {
   return dx * dy + dy * dz + dz * dx;
 }
 
-int bvh_build(std::vector<BvhPrim>& P, int b, int e, std::vector<TNode>& T, std::vector<int32_t>& order) {
+int bvh_build(std::vector<BvhPrim>& P, int b, int e, std::vector<TNode>& T, std::vector<int32_t>& order,
+              int leaf_size = rtp::kBvhLeafSize) {
   const int me = (int)T.size();
   T.emplace_back();
   TNode nd;
@@ -415,7 +417,7 @@ int bvh_build(std::vector<BvhPrim>& P, int b, int e, std::vector<TNode>& T, std:
       chi[k] = std::max(chi[k], P[i].cen[k]);
     }
   const int n = e - b;
-  if (n <= rtp::kBvhLeafSize) {
+  if (n <= leaf_size) {
     nd.first = (int)order.size();
     nd.count = n;
     for (int i = b; i < e; i++) order.push_back(P[i].idx);
@@ -470,8 +472,8 @@ int bvh_build(std::vector<BvhPrim>& P, int b, int e, std::vector<TNode>& T, std:
     mid = b + n / 2;
     nd.axis = 0;
   }
-  nd.left = bvh_build(P, b, mid, T, order);
-  nd.right = bvh_build(P, mid, e, T, order);
+  nd.left = bvh_build(P, b, mid, T, order, leaf_size);
+  nd.right = bvh_build(P, mid, e, T, order, leaf_size);
   T[me] = nd;
   return me;
 }
@@ -537,57 +539,6 @@ void bvh_flatten(const std::vector<TNode>& T, int t, int oct, const std::vector<
   out[me] = nd;
 }
 
-// The LDS walk's layout of the SAH tree (rtp_layout.hpp LdsBvhNode): nodes
-// numbered breadth-first with each inner node's children allocated as an
-// adjacent pair.  Only for trees whose leaves hold one sphere each and that
-// fit kLdsBvhMaxNodes; returns false otherwise.
-bool bvh_lds_layout(const std::vector<TNode>& T, const std::vector<int32_t>& order,
-                    const std::vector<rtp::DevSphere>& sph, std::vector<rtp::LdsBvhNode>& out) {
-  out.clear();
-  if (T.empty() || (int)T.size() > rtp::kLdsBvhMaxNodes) return false;
-  for (const TNode& t : T)
-    if (t.left < 0 && t.count != 1) return false;
-  out.resize(T.size());
-  std::vector<int> slot_of(T.size(), -1), queue{0};
-  slot_of[0] = 0;
-  int next = 1;
-  auto fill = [&](int t, int me, int parent, int paxis, int right) {
-    rtp::LdsBvhNode& nd = out[me];
-    std::memset(&nd, 0, sizeof(nd));
-    const TNode& s = T[t];
-    int32_t link = (parent & 0xffff) | (s.axis & 3) << 16 | (paxis & 3) << 18 | (right & 1) << 20;
-    if (s.left < 0) {
-      const rtp::DevSphere& S = sph[order[s.first]];
-      std::memcpy(nd.a, S.c, sizeof(nd.a));
-      nd.b[0] = S.rr;
-      const int32_t orig = order[s.first];
-      std::memcpy(&nd.b[1], &orig, sizeof(orig));
-      link |= 1 << 21;
-      nd.left = -1;
-    } else {
-      std::memcpy(nd.a, s.lo, sizeof(nd.a));
-      std::memcpy(nd.b, s.hi, sizeof(nd.b));
-    }
-    nd.link = link;
-  };
-  fill(0, 0, 0xffff, 0, 0);
-  for (size_t qi = 0; qi < queue.size(); qi++) {
-    const int t = queue[qi], me = slot_of[t];
-    const TNode& s = T[t];
-    if (s.left < 0) continue;
-    const int L = next;
-    next += 2;
-    out[me].left = L;
-    slot_of[s.left] = L;
-    slot_of[s.right] = L + 1;
-    fill(s.left, L, me, s.axis, 0);
-    fill(s.right, L + 1, me, s.axis, 1);
-    queue.push_back(s.left);
-    queue.push_back(s.right);
-  }
-  return next == (int)T.size();
-}
-
 }  // namespace
 
 // error reporting for the other translation units of librtp.so
@@ -648,7 +599,8 @@ void rtp_destroy(rtp_context* c) {
   if (c->d_nodes) (void)hipFree(c->d_nodes);
   if (c->d_sph_geom) (void)hipFree(c->d_sph_geom);
   if (c->d_sph_all) (void)hipFree(c->d_sph_all);
-  if (c->d_lnodes) (void)hipFree(c->d_lnodes);
+  for (void* p : {(void*)c->d_lw_nodes, (void*)c->d_lw_cidx, (void*)c->d_lw_sph, (void*)c->d_lw_orig})
+    if (p) (void)hipFree(p);
   if (c->d_cnodes) (void)hipFree(c->d_cnodes);
   if (c->d_cidx) (void)hipFree(c->d_cidx);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -783,7 +735,10 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
   }
   std::vector<rtp::BvhNode> nodes;
   std::vector<rtp::DevSphereG> geom;
-  std::vector<rtp::LdsBvhNode> lnodes;
+  // the LDS walk's tree (kLdsWalkLeaf) in BvhNode form, its leaf order and size
+  std::vector<rtp::BvhNode> lw_nodes;
+  std::vector<int32_t> lw_order;
+  int lw_per_oct = 0;
   if (!use_bvh) {
     for (int k = 0; k < s->n_spheres; k++) h->spheres[k] = sph[k];
   } else if (gpu_build) {
@@ -803,15 +758,10 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
       }
       P[k].idx = k;
     }
+    const std::vector<BvhPrim> P0 = P;  // (bvh_build reorders P)
     std::vector<int32_t> order;
     std::vector<TNode> tree;
     bvh_build(P, 0, s->n_spheres, tree, order);
-    // the LDS walk (rtp_render_pool_lds) is opt-in, RTP_BVH_LDS=1: on C3 it
-    // ran 1118 ms against the global threaded walk's 591 (32 spp, r03f):
-    // 48% more VALU instructions for the stackless state machine, and lanes
-    // diverge as much as on the global walk (13 vs 17 of 64 per instruction)
-    const char* le = getenv("RTP_BVH_LDS");
-    if (le && le[0] == '1' && bvh_lds_layout(tree, order, sph, lnodes)) h->n_lnodes = (int32_t)lnodes.size();
     // inner nodes above this depth are not emitted (bvh_flatten; RTP_BVH_DROP overrides)
     int drop = kBvhDropDepth;
     float drop_sa = kBvhDropArea;
@@ -823,6 +773,32 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
       bvh_flatten(tree, 0, oct, order, sph, one, 0, drop, drop_sa);
       per_oct = (int)one.size();  // (the same nodes are dropped in every octant's order)
       nodes.insert(nodes.end(), one.begin(), one.end());
+    }
+    // The LDS walk's tree (opt-in, RTP_BVH_LDS=1): leaves of up to
+    // kLdsWalkLeaf spheres, flattened the same way, used when its 8 copies
+    // plus the leaf spheres fit the block's LDS (the stats build and planned
+    // launches walk the global tree).  On C3 at 16 spp (r04h/r04i, kernel ms):
+    // LDS walk 324, the global walk over the same leaves-of-6 tree 349, the
+    // global walk over the leaves-of-1 tree 186 -- the LDS copy saves 7% of the
+    // texture-path gathers' cost, the bigger leaves it needs to fit cost 88%
+    // (10 exact sphere tests per ray instead of 4: DESIGN.md 4.2).
+    const char* le = getenv("RTP_BVH_LDS");
+    if (le && le[0] == '1') {
+      std::vector<BvhPrim> P2 = P0;
+      std::vector<TNode> tree2;
+      bvh_build(P2, 0, s->n_spheres, tree2, lw_order, rtp::kLdsWalkLeaf);
+      for (int oct = 0; oct < 8; oct++) {
+        std::vector<rtp::BvhNode> one;
+        bvh_flatten(tree2, 0, oct, lw_order, sph, one, 0, drop, drop_sa);
+        lw_per_oct = (int)one.size();
+        lw_nodes.insert(lw_nodes.end(), one.begin(), one.end());
+      }
+      const int64_t bytes = (int64_t)16 * (8 * (int64_t)lw_per_oct + (int64_t)lw_order.size());
+      if (bytes > rtp_lds_walk_capacity()) {
+        lw_nodes.clear();
+        lw_order.clear();
+        lw_per_oct = 0;
+      }
     }
     geom.resize(order.size());
     for (size_t j = 0; j < order.size(); j++) {
@@ -877,8 +853,9 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     if (e == hipSuccess) e = hipEventSynchronize(c->done);
     c->pending = false;
   }
-  for (void** p : {(void**)&c->d_nodes, (void**)&c->d_sph_geom, (void**)&c->d_sph_all, (void**)&c->d_lnodes,
-                   (void**)&c->d_cnodes, (void**)&c->d_cidx})
+  for (void** p : {(void**)&c->d_nodes, (void**)&c->d_sph_geom, (void**)&c->d_sph_all, (void**)&c->d_cnodes,
+                   (void**)&c->d_cidx, (void**)&c->d_lw_nodes, (void**)&c->d_lw_cidx, (void**)&c->d_lw_sph,
+                   (void**)&c->d_lw_orig})
     if (*p && e == hipSuccess) {
       e = hipFree(*p);
       *p = nullptr;
@@ -917,15 +894,36 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
       e = hipMemcpy(c->d_sph_geom, geom.data(), geom.size() * sizeof(rtp::DevSphereG), hipMemcpyHostToDevice);
     if (e == hipSuccess)
       e = hipMemcpy(c->d_sph_all, sph.data(), sph.size() * sizeof(rtp::DevSphere), hipMemcpyHostToDevice);
-    if (e == hipSuccess && !lnodes.empty()) {
-      e = hipMalloc(&c->d_lnodes, lnodes.size() * sizeof(rtp::LdsBvhNode));
-      if (e == hipSuccess)
-        e = hipMemcpy(c->d_lnodes, lnodes.data(), lnodes.size() * sizeof(rtp::LdsBvhNode), hipMemcpyHostToDevice);
-    }
     h->nodes = c->d_nodes;
     h->sph_geom = c->d_sph_geom;
     h->sph_all = c->d_sph_all;
-    h->lnodes = c->d_lnodes;
+    if (e == hipSuccess && lw_per_oct > 0) {  // the LDS walk's tree: compacted like the global one
+      const int64_t total = (int64_t)8 * lw_per_oct, ns = (int64_t)lw_order.size();
+      std::vector<float> lsph(4 * ns);
+      for (int64_t j = 0; j < ns; j++) {
+        const rtp::DevSphere& S = sph[lw_order[j]];
+        lsph[4 * j] = S.c[0], lsph[4 * j + 1] = S.c[1], lsph[4 * j + 2] = S.c[2], lsph[4 * j + 3] = S.rr;
+      }
+      rtp::BvhNode* d_tmp = nullptr;
+      e = hipMalloc(&d_tmp, (size_t)total * sizeof(rtp::BvhNode));
+      if (e == hipSuccess) e = hipMalloc(&c->d_lw_nodes, (size_t)total * 16);
+      if (e == hipSuccess) e = hipMalloc(&c->d_lw_cidx, (size_t)total * sizeof(int32_t));
+      if (e == hipSuccess) e = hipMalloc(&c->d_lw_sph, (size_t)ns * 16);
+      if (e == hipSuccess) e = hipMalloc(&c->d_lw_orig, (size_t)ns * sizeof(int32_t));
+      if (e == hipSuccess)
+        e = hipMemcpy(d_tmp, lw_nodes.data(), (size_t)total * sizeof(rtp::BvhNode), hipMemcpyHostToDevice);
+      if (e == hipSuccess) e = hipMemcpy(c->d_lw_sph, lsph.data(), (size_t)ns * 16, hipMemcpyHostToDevice);
+      if (e == hipSuccess)
+        e = hipMemcpy(c->d_lw_orig, lw_order.data(), (size_t)ns * sizeof(int32_t), hipMemcpyHostToDevice);
+      if (e == hipSuccess) e = rtp_compact_bvh(d_tmp, total, c->d_lw_nodes, c->d_lw_cidx, nullptr);
+      if (d_tmp) (void)hipFree(d_tmp);
+      h->lw_nodes = c->d_lw_nodes;
+      h->lw_cidx = c->d_lw_cidx;
+      h->lw_sph = c->d_lw_sph;
+      h->lw_orig = c->d_lw_orig;
+      h->n_lw_nodes = lw_per_oct;
+      h->n_lw_sph = (int32_t)ns;
+    }
   }
   if (use_bvh && e == hipSuccess) {  // the walks' compact copy of the octant arrays
     const int64_t total = (int64_t)8 * h->n_nodes;
@@ -936,7 +934,7 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     h->cidx = c->d_cidx;
   }
   if (e == hipSuccess) e = hipMemcpy(c->d_scene, h, sizeof(*h), hipMemcpyHostToDevice);
-  c->n_lnodes = h->n_lnodes;
+  c->lw_bytes = h->n_lw_nodes > 0 ? 16 * (8 * h->n_lw_nodes + h->n_lw_sph) : 0;
   delete h;
   c->use_bvh = use_bvh;
   if (e != hipSuccess) return hip_fail(e, "rtp_set_scene upload");
@@ -1023,7 +1021,7 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
   // 1 the global threaded walk (also for the diagnostics build and wave plans)
   const char* stats_env = getenv("RTP_DEBUG_STATS");
   const bool stats_on = stats_env && stats_env[0] == '1';
-  const int bvh = !c->use_bvh ? 0 : (c->n_lnodes > 0 && !stats_on && !d_wave_begin) ? 2 : 1;
+  const int bvh = !c->use_bvh ? 0 : (c->lw_bytes > 0 && !stats_on && !d_wave_begin) ? 2 : 1;
   int64_t lanes = rtp_plan_history_lanes(npix, spp, bvh, &variant, &waves);
   if (d_wave_begin) {  // a planned launch: the caller's waves
     if (variant != 2 || c->use_bvh || tile)
@@ -1069,7 +1067,7 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
     }
   }
   if (kernel_ms) HIP_TRY(hipEventRecord(c->ev0, stream));
-  HIP_TRY(rtp_launch_render(c->d_scene, &p, variant, waves, bvh, stream, c->n_lnodes));
+  HIP_TRY(rtp_launch_render(c->d_scene, &p, variant, waves, bvh, stream, c->lw_bytes));
   HIP_TRY(hipEventRecord(c->done, stream));
   c->pending = true;
   if (kernel_ms) {
@@ -1321,6 +1319,11 @@ rtp_status rtp_debug_closest_hit(rtp_context* c, const float* rays, int64_t n, u
   if (dout) (void)hipFree(dout);
   if (e != hipSuccess) return hip_fail(e, "rtp_debug_closest_hit");
   return RTP_OK;
+}
+
+int32_t rtp_sphere_walk(rtp_context* c) {
+  if (!c || !c->has_scene || !c->use_bvh) return 0;
+  return c->lw_bytes > 0 ? 2 : 1;
 }
 
 // Diagnostics: exhaustive device check of a fast arithmetic sequence (kind,

@@ -160,15 +160,20 @@ RTP_DEV float slab_rcp(float v) { return __builtin_amdgcn_rcpf(fabsf(v) < 1e-20f
 struct BvhRay {
   GU4* nodes;
   GI32* cidx;
+  GI32* orig;           // LDS walk: the scene index of a leaf-order sphere position (kind 3 hits)
   float ix, iy, iz;     // 1/d (clamped)
   float ox, oy, oz;     // -o/d
 };
+RTP_DEV int ray_octant(f3 d) { return (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0); }
+// kLds: the LDS walk's tree (its global side tables; the nodes are read from LDS)
+template <bool kLds = false>
 RTP_DEV BvhRay bvh_ray(const DevScene* __restrict__ sc, f3 o, f3 d) {
-  const int oct = (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0);
-  const int64_t base = (int64_t)oct * sc->n_nodes;
+  const int oct = ray_octant(d);
+  const int64_t base = (int64_t)oct * (kLds ? sc->n_lw_nodes : sc->n_nodes);
   BvhRay R;
-  R.nodes = (GU4*)(sc->cnodes + 4 * base);
-  R.cidx = (GI32*)(sc->cidx + base);
+  R.nodes = (GU4*)((kLds ? sc->lw_nodes : sc->cnodes) + 4 * base);
+  R.cidx = (GI32*)((kLds ? sc->lw_cidx : sc->cidx) + base);
+  R.orig = (GI32*)sc->lw_orig;
   R.ix = slab_rcp(d.x);
   R.iy = slab_rcp(d.y);
   R.iz = slab_rcp(d.z);
@@ -178,33 +183,33 @@ RTP_DEV BvhRay bvh_ray(const DevScene* __restrict__ sc, f3 o, f3 d) {
   return R;
 }
 // During a walk a sphere hit is h.kind == 2 with h.idx the leaf's node (the
-// sphere's scene index is cidx[node]); bvh_resolve turns it into kind 1 with
-// the scene index.  Kind 1 hits (multi-sphere leaves) carry the index.
-RTP_DEV int bvh_hit_index(const Hit& h, GI32* cidx) { return h.kind == 2 ? cidx[h.idx] : h.idx; }
-RTP_DEV void bvh_resolve(Hit& h, GI32* cidx) {
-  if (h.kind == 2) {
-    h.idx = cidx[h.idx];
+// sphere's scene index is cidx[node]), or, in the LDS walk's multi-sphere
+// leaves, h.kind == 3 with h.idx the sphere's leaf-order position (scene index
+// orig[pos]); bvh_resolve turns either into kind 1 with the scene index.
+// Kind 1 hits (the global walk's multi-sphere leaves) carry the index.
+RTP_DEV int bvh_hit_index(const Hit& h, const BvhRay& R) {
+  return h.kind == 2 ? R.cidx[h.idx] : h.kind == 3 ? R.orig[h.idx] : h.idx;
+}
+RTP_DEV void bvh_resolve(Hit& h, const BvhRay& R) {
+  if (h.kind >= 2) {
+    h.idx = bvh_hit_index(h, R);
     h.kind = 1;
   }
 }
-// the closest-sphere update: the (t, scene index) minimum, quads winning t ties
-RTP_DEV void bvh_accept_leaf(Hit& h, float t, int node, GI32* cidx) {
+// the closest-sphere update: the (t, scene index) minimum, quads winning t
+// ties; `ref` is the hit's kind-`kind` reference, `orig` reads its scene index
+// (only for an exact tie between spheres: rare)
+template <class Orig>
+RTP_DEV void bvh_accept(Hit& h, float t, int kind, int ref, const BvhRay& R, Orig orig) {
   if (t < h.t) {
     h.t = t;
-    h.kind = 2;
-    h.idx = node;
-  } else if (t == h.t && h.kind >= 1) {  // an exact tie between spheres (rare): the smaller scene index
-    if (cidx[node] < bvh_hit_index(h, cidx)) {
-      h.kind = 2;
-      h.idx = node;
+    h.kind = kind;
+    h.idx = ref;
+  } else if (t == h.t && h.kind >= 1) {
+    if (orig() < bvh_hit_index(h, R)) {
+      h.kind = kind;
+      h.idx = ref;
     }
-  }
-}
-RTP_DEV void bvh_accept_orig(Hit& h, float t, int orig, GI32* cidx) {
-  if (t < h.t || (t == h.t && h.kind >= 1 && orig < bvh_hit_index(h, cidx))) {
-    h.t = t;
-    h.kind = 1;
-    h.idx = orig;
   }
 }
 RTP_DEV float half_lo(uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v & 0xffffu)); }
@@ -214,12 +219,19 @@ RTP_DEV float half_hi(uint32_t v) { return (float)__builtin_bit_cast(_Float16, (
 // done).  A sphere leaf runs the exact root test (no box); an inner node's
 // box (padded on the host, rounded outward to half precision, compared with
 // slack here) only culls.
-RTP_DEV int bvh_visit(GF4* __restrict__ geom_g, const BvhRay& R, f3 o, f3 d, u4v v, int ni, Hit& h) {
+// kLds: the LDS walk (rtp_render_pool_lds): a multi-sphere leaf's spheres
+// are (centre, r^2) float4s in the block's LDS (lsph), else 32-byte
+// DevSphereG records in global memory (geom_g).
+typedef const __attribute__((address_space(3))) f4v LF4;
+typedef const __attribute__((address_space(3))) u4v LU4;
+template <bool kLds = false>
+RTP_DEV int bvh_visit(GF4* __restrict__ geom_g, LF4* __restrict__ lsph, const BvhRay& R, f3 o, f3 d, u4v v, int ni,
+                      Hit& h) {
   if ((int32_t)v.w < 0) {  // a sphere leaf: centre, r^2
     float t;
     if (sphere_root(o, d, 0.001f, mk(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z)),
                     __uint_as_float(v.w & ~kCBvhSphereBit), t))
-      bvh_accept_leaf(h, t, ni, R.cidx);
+      bvh_accept(h, t, 2, ni, R, [&] { return R.cidx[ni]; });
     return ni + 1;
   }
   const float x0 = __builtin_fmaf(half_lo(v.x), R.ix, R.ox), x1 = __builtin_fmaf(half_hi(v.y), R.ix, R.ox);
@@ -233,10 +245,15 @@ RTP_DEV int bvh_visit(GF4* __restrict__ geom_g, const BvhRay& R, f3 o, f3 d, u4v
   if (hit && leaf) {  // a multi-sphere leaf: its spheres in leaf order
     const int first = (int)((v.w & ~kCBvhLeafBit) >> 3), cnt = (int)(v.w & 7u);
     for (int j = first; j < first + cnt; j++) {
-      const f4v g0 = geom_g[2 * j], g1 = geom_g[2 * j + 1];  // c, rr | orig
       float t;
-      if (sphere_root(o, d, 0.001f, mk(g0.x, g0.y, g0.z), g0.w, t))
-        bvh_accept_orig(h, t, __float_as_int(g1.x), R.cidx);
+      if constexpr (kLds) {
+        const f4v g0 = lsph[j];  // c, rr
+        if (sphere_root(o, d, 0.001f, mk(g0.x, g0.y, g0.z), g0.w, t)) bvh_accept(h, t, 3, j, R, [&] { return R.orig[j]; });
+      } else {
+        const f4v g0 = geom_g[2 * j], g1 = geom_g[2 * j + 1];  // c, rr | orig
+        if (sphere_root(o, d, 0.001f, mk(g0.x, g0.y, g0.z), g0.w, t))
+          bvh_accept(h, t, 1, __float_as_int(g1.x), R, [&] { return __float_as_int(g1.x); });
+      }
     }
   }
   return (hit || leaf) ? ni + 1 : (int)v.w;
@@ -253,81 +270,11 @@ RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
   int ni = 0;
   u4v v = R.nodes[0];
   while (ni < nn) {
-    const int next = bvh_visit(geom_g, R, o, d, v, ni, h);
+    const int next = bvh_visit(geom_g, nullptr, R, o, d, v, ni, h);
     if (next < nn) v = R.nodes[next];
     ni = next;
   }
-  bvh_resolve(h, R.cidx);
-}
-
-// The same closest-sphere search over the block's LDS copy of the tree
-// (LdsBvhNode, one copy for every direction): a stackless walk with parent
-// links (Hapala, Sassa, Pfister 2011).  State fromParent: `cur` was entered
-// from its parent (it is the near child); fromSibling: it is the far child,
-// entered after the near one's subtree; fromChild: `cur`'s subtree is done.
-// A node is tested on entry -- the slab test against [0, best t] with the
-// slack of spheres_bvh, or, for a leaf, its sphere -- and the walk descends
-// into a hit inner node's near child (on the side the ray comes from along
-// its split axis).  Each step is one 32-byte LDS read.
-RTP_DEV void spheres_bvh_lds(const LdsBvhNode* __restrict__ nodes, f3 o, f3 d, Hit& h) {
-  const float tmin = 0.001f;
-  const float ix = __builtin_amdgcn_rcpf(fabsf(d.x) < 1e-20f ? copysignf(1e-20f, d.x) : d.x);
-  const float iy = __builtin_amdgcn_rcpf(fabsf(d.y) < 1e-20f ? copysignf(1e-20f, d.y) : d.y);
-  const float iz = __builtin_amdgcn_rcpf(fabsf(d.z) < 1e-20f ? copysignf(1e-20f, d.z) : d.z);
-  const uint32_t neg = (d.x < 0.f ? 1u : 0u) | (d.y < 0.f ? 2u : 0u) | (d.z < 0.f ? 4u : 0u);
-  auto accept = [&](float t, int orig) {
-    if (t < h.t || (t == h.t && h.kind == 1 && orig < h.idx)) {
-      h.t = t;
-      h.kind = 1;
-      h.idx = orig;
-    }
-  };
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  const f4v* nv = reinterpret_cast<const f4v*>(nodes);
-  enum { kFromParent = 0, kFromSibling = 1, kFromChild = 2 };
-  int cur = 0, state = kFromParent;
-  for (;;) {
-    const f4v A = nv[2 * cur], B = nv[2 * cur + 1];
-    const int link = __float_as_int(A.w), left = __float_as_int(B.w);
-    const bool right = (link >> 20) & 1;
-    if (state == kFromChild) {
-      if (cur == 0) break;
-      // done with cur's subtree: its far sibling next if cur is the near child
-      const bool was_near = (uint32_t)right == ((neg >> ((link >> 18) & 3)) & 1u);
-      if (was_near) {
-        cur = right ? cur - 1 : cur + 1;
-        state = kFromSibling;
-      } else {
-        cur = link & 0xffff;
-      }
-      continue;
-    }
-    bool descend = false;
-    if ((link >> 21) & 1) {  // a leaf: its sphere
-      float t;
-      if (sphere_root(o, d, tmin, mk(A.x, A.y, A.z), B.x, t)) accept(t, __float_as_int(B.y));
-    } else {
-      const float x0 = (A.x - o.x) * ix, x1 = (B.x - o.x) * ix;
-      const float y0 = (A.y - o.y) * iy, y1 = (B.y - o.y) * iy;
-      const float z0 = (A.z - o.z) * iz, z1 = (B.z - o.z) * iz;
-      const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
-      const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
-      const float slack = 1e-5f * fabsf(tf) + 1e-7f;
-      descend = tn <= tf + slack && tf >= 0.0f && tn <= h.t * 1.00001f + 1e-7f;
-    }
-    if (descend) {
-      cur = left + (int)((neg >> ((link >> 16) & 3)) & 1u);
-      state = kFromParent;
-    } else if (cur == 0) {
-      break;  // the root itself missed (or is the only leaf)
-    } else if (state == kFromParent) {
-      cur = right ? cur - 1 : cur + 1;
-      state = kFromSibling;
-    } else {
-      cur = link & 0xffff;
-      state = kFromChild;
-    }
-  }
+  bvh_resolve(h, R);
 }
 
 // qshade: the block's LDS copy of the quads' shading data (n, alb, mt) so
@@ -478,9 +425,9 @@ RTP_DEV bool quad_hit_axis(const PreExact& E, f3 o, f3 d, float& t_out) {
 
 // kSpheres = false: the quads only (the pool kernel's resumable sphere-BVH
 // walk, spheres_bvh_step, continues from the quads' hit).
-template <bool kBvh, bool kLdsBvh = false, bool kSpheres = true>
+template <bool kBvh, bool kSpheres = true>
 RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefilter,
-                        uint32_t* full_out, const float* lds_prex, const LdsBvhNode* lds_bvh = nullptr) {
+                        uint32_t* full_out, const float* lds_prex) {
   Hit h{3.40282347e+38f, -1, 0};
   const float tmin = 0.001f;
   // the (t, orig) key minimum: the order the kinds are scanned in is free
@@ -548,8 +495,6 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
   }
   static_assert(kQuadKinds == 11, "closest_hit scans every kind");
   if constexpr (!kSpheres) {
-  } else if constexpr (kLdsBvh) {
-    spheres_bvh_lds(lds_bvh, o, d, h);
   } else if constexpr (kBvh) {
     spheres_bvh(sc, o, d, h);
   } else {
@@ -622,16 +567,15 @@ RTP_DEV void dbg_add(unsigned long long* gdbg, int c, unsigned long long v) { at
 template <bool kBvh, bool kDeferDead>
 RTP_DEV int shade_hit(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3& emit, float4* __restrict__ hist_d,
                       int D, const float* qshade, const Hit h, unsigned long long* dbg = nullptr);
-template <bool kBvh, bool kDeferDead = false, bool kLdsBvh = false>
+template <bool kBvh, bool kDeferDead = false>
 RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3& emit, float4* __restrict__ hist_d,
-                   int D, unsigned long long* dbg, const float* qshade, const LdsBvhNode* lds_bvh = nullptr,
-                   unsigned long long* gdbg = nullptr) {
+                   int D, unsigned long long* dbg, const float* qshade, unsigned long long* gdbg = nullptr) {
   const bool st = dbg != nullptr;
   const unsigned long long t0 = stamp(st);
   const f3 org = ps.org, dir = ps.dir;
   // intersect + CollectIntersecttWorklet (SurfaceWorklets.h:104-109)
   uint32_t fb = 0;  // (stats) 1: this lane ran the exact scan of the prefiltered quads
-  Hit h = closest_hit<kBvh, kLdsBvh>(sc, org, dir, true, st ? &fb : nullptr, qshade + kPrexLdsOffset, lds_bvh);
+  Hit h = closest_hit<kBvh>(sc, org, dir, true, st ? &fb : nullptr, qshade + kPrexLdsOffset);
   if (st) {
     const unsigned long long m = __ballot(fb == 1u);
     dbg[kDbgFallbackSteps] += m ? 1 : 0;
@@ -984,7 +928,8 @@ typedef const __attribute__((address_space(1))) uint32_t GU32;
 // [wave_begin[w], wave_begin[w+1]) -- up to kPool of them, grouped by their
 // expected cost -- instead of the interleaved entries j * n_waves + w.
 // The pool kernel's body; kWPB waves per block, kLdsBvh: the sphere BVH is
-// walked out of the block's LDS copy (s_bvh, rtp_render_pool_lds).
+// walked out of the block's LDS copy (s_bvh: the LDS walk's compact nodes,
+// then its leaf spheres; rtp_render_pool_lds).
 // kSteal: a launch with more entries than its waves' pools hold (C3, C4,
 // C5 on one GPU).  The waves are the resident ones; a slot whose pixel has
 // all its samples writes the pixel out and claims the next unclaimed entry
@@ -992,18 +937,20 @@ typedef const __attribute__((address_space(1))) uint32_t GU32;
 // waves of 128 pixels each running in generations with a tail per wave.
 template <bool kStats, bool kBvh, bool kTiles, bool kPlan, int kWPB, bool kLdsBvh, bool kSteal = false>
 __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const KParams& p, int n_waves,
-                                          unsigned char* smem, float* s_qshade, LdsBvhNode* s_bvh,
+                                          unsigned char* smem, float* s_qshade, uint32_t* s_bvh,
                                           uint32_t* s_entry_all = nullptr) {
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
   const int w = blockIdx.x * kWPB + wib;  // global wave id
   // the quads' shading data into LDS (the block's only barrier, before any wave leaves)
   fill_qshade(sc, s_qshade);  // (n_quads <= kMaxQuads = kLdsQuads)
-  if constexpr (kLdsBvh) {    // and the sphere BVH (n_lnodes <= kLdsBvhMaxNodes, checked on the host)
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    const auto* src = (const __attribute__((address_space(1))) f4v*)sc->lnodes;
-    f4v* dst = reinterpret_cast<f4v*>(s_bvh);
-    for (int i = threadIdx.x; i < 2 * sc->n_lnodes; i += blockDim.x) dst[i] = src[i];
+  if constexpr (kLdsBvh) {  // and the LDS walk's tree (its size checked on the host: rtp_lds_walk_capacity)
+    const int nn = 8 * sc->n_lw_nodes, ns = sc->n_lw_sph;
+    u4v* dst = reinterpret_cast<u4v*>(s_bvh);
+    GU4* const gn = (GU4*)sc->lw_nodes;
+    GU4* const gs = (GU4*)sc->lw_sph;
+    for (int i = threadIdx.x; i < nn; i += blockDim.x) dst[i] = gn[i];
+    for (int i = threadIdx.x; i < ns; i += blockDim.x) dst[nn + i] = gs[i];
   }
   __syncthreads();
   if (w >= n_waves) return;  // whole wave leaves; no block-level barriers follow
@@ -1094,7 +1041,7 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
   // to its end inside one iteration); now a long walk no longer holds the
   // other 63 lanes.  The walk is the same walk (same nodes, same order, same
   // running minimum), so the hit is bit-identical.
-  constexpr bool kWalk = kBvh && !kLdsBvh;
+  constexpr bool kWalk = kBvh;
   int wni = -1;                             // the path's next BVH node; -1: its quads are not scanned yet
   Hit wh{3.40282347e+38f, -1, 0};           // its closest hit so far
   Path ps;
@@ -1320,9 +1267,9 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
     unsigned long long tbnc = ta;
     bool shade = has_path;
     if constexpr (kWalk) {
-      const int nn = sc->n_nodes;
+      const int nn = kLdsBvh ? sc->n_lw_nodes : sc->n_nodes;
       if (has_path && wni < 0) {  // a new ray: the quads first (their hit bounds the walk)
-        wh = closest_hit<false, false, false>(sc, ps.org, ps.dir, true, nullptr, s_qshade + kPrexLdsOffset);
+        wh = closest_hit<false, false>(sc, ps.org, ps.dir, true, nullptr, s_qshade + kPrexLdsOffset);
         wni = 0;
       }
       const uint64_t pm = __ballot(has_path);
@@ -1330,21 +1277,25 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
       bool walking = has_path && wni < nn;
       if (__ballot(walking)) {
         const f3 o = ps.org, d = ps.dir;
-        const BvhRay R = bvh_ray(sc, o, d);
+        const BvhRay R = bvh_ray<kLdsBvh>(sc, o, d);
         GF4* __restrict__ geom_g = (GF4*)sc->sph_geom;
+        // the LDS walk: this octant's copy of the nodes, then the leaf spheres
+        LU4* const lnodes = (LU4*)s_bvh + (kLdsBvh ? ray_octant(d) * nn : 0);
+        LF4* const lsph = (LF4*)s_bvh + (kLdsBvh ? 8 * nn : 0);
+        auto node = [&](int i) { return kLdsBvh ? lnodes[i] : R.nodes[i]; };
         u4v v = u4v{0u, 0u, 0u, 0u};
-        if (walking) v = R.nodes[wni];
+        if (walking) v = node(wni);
         for (;;) {
           const uint64_t wm = __ballot(walking);
           if (wm == 0 || __popcll(pm & ~wm) >= need) break;
           if (walking) {
-            const int next = bvh_visit(geom_g, R, o, d, v, wni, wh);
+            const int next = bvh_visit<kLdsBvh>(geom_g, lsph, R, o, d, v, wni, wh);
             walking = next < nn;
-            if (walking) v = R.nodes[next];
+            if (walking) v = node(next);
             wni = next;
           }
         }
-        if (has_path && !walking) bvh_resolve(wh, R.cidx);
+        if (has_path && !walking) bvh_resolve(wh, R);
       }
       shade = has_path && !walking;
       if (want_dbg) dbg[kDbgCyclesIntersect] += stamp(want_dbg) - ta;
@@ -1356,8 +1307,8 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
         res = shade_hit<kBvh, true>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D, s_qshade, wh);
         wni = -1;
       } else {
-        res = bounce<kBvh, true, kLdsBvh>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D,
-                                          want_dbg ? dbg : nullptr, s_qshade, s_bvh, gdbg);
+        res = bounce<kBvh, true>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D, want_dbg ? dbg : nullptr,
+                                 s_qshade, gdbg);
       }
       tbnc = stamp(want_dbg);
       if (res == kAlive && ps.d < D - 1) {
@@ -1468,21 +1419,28 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
   }
 }
 
-// Scenes whose sphere BVH fits the LDS (LdsBvhNode, <= kLdsBvhMaxNodes):
+// Scenes whose LDS walk tree fits (DevScene::lw_nodes, rtp_lds_walk_capacity):
 // one 16-wave block per CU (4 waves per SIMD, <= 128 VGPRs) shares one LDS
-// copy of the tree -- dynamic LDS after the waves' pools and the quad tables.
-template <bool kTiles>
+// copy of the tree -- dynamic LDS after the waves' pools, the quad tables and
+// (kSteal) the slots' entries.
+template <bool kTiles, bool kSteal>
 __global__ void __launch_bounds__(64 * kLdsBvhWavesPerBlock, 1) __attribute__((amdgpu_num_vgpr(128)))
     rtp_render_pool_lds(const DevScene* __restrict__ sc, KParams p, int n_waves) {
   __shared__ __align__(16) unsigned char smem[kLdsBvhWavesPerBlock * kPool * kSlotBytes];
   __shared__ __align__(16) float s_qshade[kQTableFloats];
-  extern __shared__ __align__(16) unsigned char s_dyn[];
-  pool_body<false, true, kTiles, false, kLdsBvhWavesPerBlock, true>(sc, p, n_waves, smem, s_qshade,
-                                                                    reinterpret_cast<LdsBvhNode*>(s_dyn));
+  extern __shared__ __align__(16) uint32_t s_dyn[];
+  if constexpr (kSteal) {
+    __shared__ uint32_t s_entry[kLdsBvhWavesPerBlock * kPool];
+    pool_body<false, true, kTiles, false, kLdsBvhWavesPerBlock, true, true>(sc, p, n_waves, smem, s_qshade, s_dyn,
+                                                                            s_entry);
+  } else {
+    pool_body<false, true, kTiles, false, kLdsBvhWavesPerBlock, true>(sc, p, n_waves, smem, s_qshade, s_dyn);
+  }
 }
-constexpr int kLdsBvhStaticBytes = kLdsBvhWavesPerBlock * kPool * kSlotBytes + kQTableFloats * 4;
-static_assert(kLdsBvhStaticBytes + kLdsBvhMaxNodes * (int)sizeof(LdsBvhNode) <= 160 * 1024,
-              "the LDS walk's block fits the CU's 160 KiB");
+constexpr int kLdsWalkStaticBytes =
+    kLdsBvhWavesPerBlock * kPool * kSlotBytes + kQTableFloats * 4 + kLdsBvhWavesPerBlock * kPool * 4;
+constexpr int kLdsWalkDynBytes = 160 * 1024 - kLdsWalkStaticBytes;  // the tree's share of the CU's 160 KiB
+static_assert(kLdsWalkDynBytes >= 64 * 1024, "the LDS walk keeps room for a C3-size tree");
 
 // ------------------------------------------------------- diagnostics ---
 __global__ void rtp_eval_primitive_kernel(int kind, const void* in, void* out, int64_t n, const uint32_t* tab,
@@ -1608,17 +1566,28 @@ int resident_blocks_per_cu() {
     nb = 1;
   return nb;
 }
+// (the occupancy of the LDS walk's instances at the largest tree: one block
+// per CU; also sets their dynamic-LDS limit)
 int lds_bvh_resident_blocks_per_cu() {
-  const int dyn = rtp::kLdsBvhMaxNodes * (int)sizeof(rtp::LdsBvhNode);
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rtp::rtp_render_pool_lds<false>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rtp::rtp_render_pool_lds<true>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
-  int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtp::rtp_render_pool_lds<false>,
-                                                   64 * rtp::kLdsBvhWavesPerBlock, dyn) != hipSuccess || nb <= 0)
-    nb = 1;
-  return nb;
+  static int cached = -1;
+  if (cached > 0) return cached;
+  const int dyn = rtp::kLdsWalkDynBytes;
+  const void* k[4] = {reinterpret_cast<const void*>(rtp::rtp_render_pool_lds<false, false>),
+                      reinterpret_cast<const void*>(rtp::rtp_render_pool_lds<true, false>),
+                      reinterpret_cast<const void*>(rtp::rtp_render_pool_lds<false, true>),
+                      reinterpret_cast<const void*>(rtp::rtp_render_pool_lds<true, true>)};
+  for (const void* f : k) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+  auto occ = [dyn](auto kernel) {
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, 64 * rtp::kLdsBvhWavesPerBlock, dyn) != hipSuccess ||
+        b <= 0)
+      b = 1;
+    return b;
+  };
+  const int nb = std::min(std::min(occ(rtp::rtp_render_pool_lds<false, false>), occ(rtp::rtp_render_pool_lds<true, false>)),
+                          std::min(occ(rtp::rtp_render_pool_lds<false, true>), occ(rtp::rtp_render_pool_lds<true, true>)));
+  cached = nb;
+  return cached;
 }
 // bvh: 0 no sphere BVH, 1 the global threaded walk, 2 the LDS walk
 int pool_resident_waves(bool stats, int bvh) {
@@ -1732,11 +1701,15 @@ int steal_resident_waves(int bvh) {
 // resident waves' pools hold: the resident waves, each refilling its slots
 // from the unclaimed entries.  Returns the waves (0: no stealing).
 extern "C" int rtp_plan_steal(int64_t npix, int bvh) {
-  if (bvh == 2) return 0;  // (the LDS walk's kernel has no stealing instance)
   const int64_t resident = pool_resident_waves(false, bvh);
   if (npix <= resident * rtp::kPool) return 0;
+  if (bvh == 2) return (int)resident;  // (its instances' occupancy: lds_bvh_resident_blocks_per_cu)
   return std::min<int>((int)resident, steal_resident_waves(bvh));
 }
+
+// Bytes of LDS the LDS walk's tree may take (nodes of 8 octant copies plus
+// the leaf spheres, 16 B each): what the 16-wave block leaves of the CU's 160 KiB.
+extern "C" int rtp_lds_walk_capacity(void) { return rtp::kLdsWalkDynBytes; }
 
 extern "C" hipError_t rtp_launch_eval_closest(const rtp::DevScene* scene, const float* rays, uint32_t* out,
                                               int64_t n, int bvh, hipStream_t stream) {
@@ -1747,7 +1720,7 @@ extern "C" hipError_t rtp_launch_eval_closest(const rtp::DevScene* scene, const 
   return hipGetLastError();
 }
 extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::KParams* p, int variant, int waves,
-                                        int bvh, hipStream_t stream, int n_lnodes) {
+                                        int bvh, hipStream_t stream, int lds_bytes) {
   if (p->npix <= 0) return hipSuccess;
   if (variant == 1 && p->tile_world > 0) return hipErrorNotSupported;  // (v1 takes pixel lists or ranges)
   if (variant == 1) {
@@ -1757,13 +1730,16 @@ extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::K
     else
       hipLaunchKernelGGL(rtp::rtp_render_lockstep<false>, dim3((unsigned)grid), dim3(256), 0, stream, scene, *p);
   } else if (bvh == 2) {  // the sphere BVH walked out of LDS
-    if (p->wave_begin || n_lnodes <= 0 || n_lnodes > rtp::kLdsBvhMaxNodes) return hipErrorNotSupported;
+    if (p->wave_begin || lds_bytes <= 0 || lds_bytes > rtp::kLdsWalkDynBytes) return hipErrorNotSupported;
     (void)lds_bvh_resident_blocks_per_cu();  // (sets the kernels' dynamic-LDS limit once)
     const int blocks = (waves + rtp::kLdsBvhWavesPerBlock - 1) / rtp::kLdsBvhWavesPerBlock;
     const dim3 g((unsigned)blocks), b(64 * rtp::kLdsBvhWavesPerBlock);
-    const size_t dyn = (size_t)n_lnodes * sizeof(rtp::LdsBvhNode);
-    if (p->tile_world > 0) hipLaunchKernelGGL(rtp::rtp_render_pool_lds<true>, g, b, dyn, stream, scene, *p, waves);
-    else hipLaunchKernelGGL(rtp::rtp_render_pool_lds<false>, g, b, dyn, stream, scene, *p, waves);
+    const size_t dyn = (size_t)lds_bytes;
+    const bool steal = (int64_t)waves * rtp::kPool < p->npix;  // rtp_plan_steal
+    if (steal && p->tile_world > 0) hipLaunchKernelGGL((rtp::rtp_render_pool_lds<true, true>), g, b, dyn, stream, scene, *p, waves);
+    else if (steal) hipLaunchKernelGGL((rtp::rtp_render_pool_lds<false, true>), g, b, dyn, stream, scene, *p, waves);
+    else if (p->tile_world > 0) hipLaunchKernelGGL((rtp::rtp_render_pool_lds<true, false>), g, b, dyn, stream, scene, *p, waves);
+    else hipLaunchKernelGGL((rtp::rtp_render_pool_lds<false, false>), g, b, dyn, stream, scene, *p, waves);
   } else {
     const int blocks = (waves + rtp::kWavesPerBlock - 1) / rtp::kWavesPerBlock;
     const char* st = getenv("RTP_DEBUG_STATS");

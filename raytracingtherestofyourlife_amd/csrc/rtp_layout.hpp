@@ -125,21 +125,22 @@ constexpr uint32_t kCBvhSphereBit = 0x80000000u, kCBvhLeafBit = 0x40000000u;
 #define RTP_BVH_EMBED 1
 #endif
 
-// The same SAH tree for a walk out of LDS (rtp_kernels.hip spheres_bvh_lds):
-// ONE copy for every ray direction, the two children of an inner node
-// adjacent (left at an odd index L, right at L + 1; root 0), and every node
-// knowing its parent, its own split axis, its parent's split axis and which
-// child it is, so the walk needs neither a stack nor per-octant copies
-// (stackless traversal with parent links, Hapala et al. 2011).  Leaves hold
-// their one sphere: a = centre, b[0] = radius^2, b[1] = sphere index.
-struct alignas(16) LdsBvhNode {
-  float a[3];     // inner: box lo (padded as BvhNode's); leaf: sphere centre
-  int32_t link;   // parent (bits 0-15) | own axis << 16 | parent axis << 18 | right child << 20 | leaf << 21
-  float b[3];     // inner: box hi; leaf: r^2, sphere index (int bits), 0
-  int32_t left;   // inner: left child (right = left + 1); leaf: -1
-};
-static_assert(sizeof(LdsBvhNode) == 32, "two 16-byte LDS reads per node");
-constexpr int kLdsBvhMaxNodes = 2816;  // 88 KiB of dynamic LDS beside the 16-wave block's pools and tables
+// The same threaded walk out of LDS (rtp_render_pool_lds): a second tree
+// over the same spheres with leaves of up to kLdsWalkLeaf spheres (SAH,
+// bvh_build), flattened and compacted like the global one (8 octant copies of
+// 16-byte nodes), and its spheres in leaf order as (centre, r^2) float4s.
+// Each 16-wave block copies both into its LDS; the walk's node and leaf
+// gathers are then LDS reads instead of texture-path gathers (on C3 those held
+// TD 93% busy per CU, r03y).  Used when the copy fits beside the block's pools
+// (rtp_lds_walk_capacity(); C3: 8 x ~460 nodes + 1000 spheres = 74 KB).
+// Bigger leaves keep the eight copies small: a leaf costs one box test and
+// then its spheres' exact tests (tools/bvh_walk_sim.cpp: per C3 ray 27.5
+// visits and 10 sphere tests at leaves <= 6, 36 and 4 at leaves of 1).
+#ifndef RTP_LDS_WALK_LEAF
+#define RTP_LDS_WALK_LEAF 6
+#endif
+constexpr int kLdsWalkLeaf = RTP_LDS_WALK_LEAF;
+static_assert(kLdsWalkLeaf >= 1 && kLdsWalkLeaf <= 7, "a leaf's count has 3 bits");
 constexpr int kLdsBvhWavesPerBlock = 16;
 
 struct alignas(16) DevLights {
@@ -190,7 +191,7 @@ struct alignas(16) DevScene {
   uint32_t which_t2;  // smallest hash with which == 3
   float ior;
   int32_t n_nodes;                 // BVH scenes (n_spheres >= kBvhMinSpheres): nodes per octant copy
-  int32_t n_lnodes;                // LDS walk: nodes of lnodes (0: none)
+  int32_t n_lw_nodes;              // LDS walk: nodes per octant copy of lw_nodes (0: no LDS walk)
   // DielectricWorklet constants of ior, with the reference's float/double
   // operations (EmitWorklet.h:153-170): r0 = ((1 - ior) / (1 + ior))^2 of
   // schlick, and ni_over_nt = (float)(1.0 / ior) of a ray entering the glass
@@ -210,10 +211,15 @@ struct alignas(16) DevScene {
   int32_t pad2[2];
   PreQuad pre[kMaxPre];
   PreExact prex[kMaxPre];  // by quad position (< n_pre)
-  const LdsBvhNode* lnodes;  // the LDS walk's tree (global copy, loaded per block; n_lnodes above)
   const uint32_t* cnodes;    // 8 * n_nodes compact nodes (4 words each; kCBvhSphereBit above)
   const int32_t* cidx;       // 8 * n_nodes: a sphere leaf's scene index (else -1)
-  const void* pad_ptr;
+  // the LDS walk's tree (kLdsWalkLeaf): global copies, loaded into each block's LDS
+  const uint32_t* lw_nodes;  // 8 * n_lw_nodes compact nodes
+  const int32_t* lw_cidx;    // 8 * n_lw_nodes: an embedded sphere's scene index (else -1)
+  const float* lw_sph;       // n_lw_sph float4s (centre, r^2) in the leaf order of lw_nodes
+  const int32_t* lw_orig;    // n_lw_sph: the scene index of each
+  int32_t n_lw_sph;
+  int32_t pad3[3];
 };
 // The pool kernel's scans prefetch up to two records past the last quad or
 // prefilter record; these must stay inside DevScene (values never used).

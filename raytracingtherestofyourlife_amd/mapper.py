@@ -340,6 +340,12 @@ class Device:
 
     FF_POLICIES = {"auto": _lib.RTP_FF_TABLES_AUTO, "off": _lib.RTP_FF_TABLES_OFF, "on": _lib.RTP_FF_TABLES_ON}
 
+    def sphere_walk(self) -> str:
+        """How renders search the current scene's spheres (include/rtp.h
+        rtp_sphere_walk): 'scan', 'global' (threaded BVH in global memory) or
+        'lds' (the LDS-resident walk)."""
+        return ("scan", "global", "lds")[self._L.rtp_sphere_walk(self.handle)]
+
     def set_ff_tables(self, policy: str) -> dict:
         """RNG jump-table policy of this context (include/rtp.h rtp_set_ff_tables):
         'auto' (default), 'off', or 'on' (build now: a long-lived renderer).

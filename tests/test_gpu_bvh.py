@@ -117,25 +117,30 @@ def _oracle_scene(oracle, n, seed):
     return sc
 
 
-def test_lds_walk_matches_oracle_1200_spheres(rtp, oracle, device, monkeypatch):
-    """1200 spheres (2399 nodes: the tree fits the LDS walk, rtp_render_pool_lds)
-    against the oracle's brute-force closest hit, bit-exact."""
-    sc = _oracle_scene(oracle, 1200, 21)
+def test_lds_walk_matches_oracle_900_spheres(rtp, oracle, device, monkeypatch):
+    """900 spheres: the LDS walk's tree (opt-in; leaves <= kLdsWalkLeaf, 8
+    octant copies + leaf spheres) fits the block's LDS, so renders take
+    rtp_render_pool_lds -- against the oracle's brute-force closest hit,
+    bit-exact.  1200 spheres do not fit: those renders walk the global tree."""
+    sc = _oracle_scene(oracle, 900, 21)
     nx = ny = 256
     pix = np.sort(np.random.default_rng(8).choice(nx * ny, 512, replace=False)).astype(np.int64)
     want = oracle.render_pixels(sc, oracle.camera_setup(nx, ny), nx, ny, 8, 50, pix)
     monkeypatch.setenv("RTP_BVH_BUILD", "host")
-    monkeypatch.setenv("RTP_BVH_LDS", "1")  # (opt-in: slower than the global walk on C3, DESIGN.md 4.1)
+    monkeypatch.setenv("RTP_BVH_LDS", "1")
     set_scene_from_oracle(device, sc)
-    assert_render_equal(_render(device, rtp, nx, ny, 8, 50, pix), want, "LDS walk, 1200 spheres")
-    monkeypatch.delenv("RTP_BVH_LDS")
+    assert device.sphere_walk() == "lds"
+    assert_render_equal(_render(device, rtp, nx, ny, 8, 50, pix), want, "LDS walk, 900 spheres")
+    set_scene_from_oracle(device, _oracle_scene(oracle, 1200, 21))
+    assert device.sphere_walk() == "global"
     device.set_cornell_box(0)
+    assert device.sphere_walk() == "scan"
 
 
 def test_lds_walk_equals_global_walk_c3(rtp, device, monkeypatch):
-    """The C3 scene through the LDS walk (RTP_BVH_LDS=1, its 1999-node tree
-    fits) and the global threaded walk (the default), on a pixel list and
-    through the tile-deal instance: the same bits."""
+    """The C3 scene through the LDS walk (RTP_BVH_LDS=1: its tree fits) and
+    the global threaded walk (the default), on a pixel list and through the
+    tile-deal instance: the same bits."""
     import torch
 
     from raytracingtherestofyourlife_amd import shard
@@ -147,6 +152,7 @@ def test_lds_walk_equals_global_walk_c3(rtp, device, monkeypatch):
     for mode in ("lds", "global"):
         monkeypatch.setenv("RTP_BVH_LDS", "1" if mode == "lds" else "0")
         device.set_cornell_box(3)
+        assert device.sphere_walk() == mode
         out[mode] = _render(device, rtp, nx, ny, 8, 50, ids)
         t = torch.zeros((ids.size, 4), dtype=torch.float32, device="cuda")
         device.render_tiles_device(cam, nx, ny, 8, 50, t.data_ptr(), 1, 3, timed=True)
@@ -158,20 +164,25 @@ def test_lds_walk_equals_global_walk_c3(rtp, device, monkeypatch):
     assert_render_equal(out["global_tiles"], out["global"], "C3: global walk, tile-deal instance vs pixel list")
 
 
+@pytest.mark.parametrize("walk", ["lds", "global"])
 @pytest.mark.parametrize("drop", [0, 1, 3, 8])
-def test_dropped_top_nodes_match_oracle(rtp, oracle, device, monkeypatch, drop):
+def test_dropped_top_nodes_match_oracle(rtp, oracle, device, monkeypatch, drop, walk):
     """Inner nodes above depth `drop` left out of the walks' arrays
     (rtp_host.cpp bvh_flatten, RTP_BVH_DROP): their boxes count as hit, so the
     walk visits more nodes but finds the same (t, index) minimum -- bit-exact
-    against the oracle's brute-force closest hit (1200 spheres; 8 drops most
-    of the tree's inner levels)."""
-    sc = _oracle_scene(oracle, 1200, 33)
+    against the oracle's brute-force closest hit (900 spheres, both walks; 8
+    drops most of the tree's inner levels)."""
+    sc = _oracle_scene(oracle, 900, 33)
     nx = ny = 128
     pix = np.sort(np.random.default_rng(9).choice(nx * ny, 384, replace=False)).astype(np.int64)
     want = oracle.render_pixels(sc, oracle.camera_setup(nx, ny), nx, ny, 4, 50, pix)
     monkeypatch.setenv("RTP_BVH_BUILD", "host")
     monkeypatch.setenv("RTP_BVH_DROP", str(drop))
+    monkeypatch.setenv("RTP_BVH_LDS", "1" if walk == "lds" else "0")
     set_scene_from_oracle(device, sc)
-    assert_render_equal(_render(device, rtp, nx, ny, 4, 50, pix), want, f"sphere BVH without its top {drop} levels")
+    assert device.sphere_walk() == walk
+    assert_render_equal(_render(device, rtp, nx, ny, 4, 50, pix), want,
+                        f"sphere BVH ({walk} walk) without its top {drop} levels")
     monkeypatch.delenv("RTP_BVH_DROP")
+    monkeypatch.delenv("RTP_BVH_LDS")
     device.set_cornell_box(0)

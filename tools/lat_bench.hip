@@ -18,6 +18,14 @@
 //        5 the ray advance alone (random point / direction: the other modes' overhead)
 //        6 closest_hit's always-exact scan alone (kinds 7..10, 0)
 //        7 closest_hit's prefilter alone (axis-plane quads + the candidate's exact test)
+//        8 closest_hit SPLIT over lane pairs: lanes 2i and 2i+1 carry the same
+//          ray, each scans half of every quad group (and of the prefilter's
+//          records), the pair combines its keys with DPP swaps -- a wave
+//          carries 32 rays (the strong-scaling experiment: a short share's
+//          idle issue slots spent on halving each step's intersection)
+//        9 mode 8 + shade_hit (shaded on both lanes of the pair, like mode 1)
+//       10 check: mode 8's hit against closest_hit's on the same rays (prints
+//          the mismatch count; not a timing)
 // (built with -DRTP_DET_FALLBACK=0: the quad tests without their |det| > 2^40 branch)
 //
 // build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off -fno-fast-math
@@ -41,6 +49,125 @@ RTP_DEV f3 rand_dir(uint32_t& s) {
 }
 RTP_DEV f3 rand_point(uint32_t& s) {
   return mk(0.05f + 0.9f * randf(s), 0.05f + 0.9f * randf(s), 0.05f + 0.9f * randf(s));
+}
+
+// ---- lane-pair split of closest_hit (modes 8, 9) ----
+// swap with the pair partner (DPP quad_perm [1,0,3,2])
+RTP_DEV uint32_t pair_swap(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+}
+RTP_DEV uint64_t pair_min(uint64_t k) {
+  const uint64_t o = (uint64_t)pair_swap((uint32_t)(k >> 32)) << 32 | pair_swap((uint32_t)k);
+  return o < k ? o : k;
+}
+// quads [b, e) of kind K: this lane takes positions b + 2j + odd (an odd count
+// leaves the last quad to both lanes); the heads are selected per lane
+template <int K>
+RTP_DEV void scan_kind_split(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d, uint64_t& best, bool odd) {
+  for (int q = b; q < e; q += 2) {
+    const int qb = min(q + 1, e - 1);
+    const u16v ha = head_at(sc->quads + q), hb = head_at(sc->quads + qb);
+    u16v h;
+#pragma unroll
+    for (int i = 0; i < 16; i++) h[i] = odd ? hb[i] : ha[i];
+    const DevQuad& M = sc->quads[odd ? qb : q];  // (read only by a non-parallelogram's second triangle)
+    scan_one<K>(M, h, o, d, best);
+  }
+}
+template <int A>
+RTP_DEV void pre_axis_split(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d, float ma, float mb, uint32_t& k1,
+                            uint32_t& k2, bool odd) {
+  constexpr int B = (A + 1) % 3, C = (A + 2) % 3;
+  if (b == e) return;
+  const float inv = __builtin_amdgcn_rcpf(comp<A>(d));
+  const float oa = comp<A>(o);
+  const f2v obc = f2v{comp<B>(o), comp<C>(o)}, dbc = f2v{comp<B>(d), comp<C>(d)};
+  for (int q = b; q < e; q += 2) {
+    const int qb = min(q + 1, e - 1);
+    const PreQuad Pa = sc->pre[q], Pb = sc->pre[qb];
+    const float px = odd ? Pb.x : Pa.x, cb = odd ? Pb.cb : Pa.cb, cc = odd ? Pb.cc : Pa.cc;
+    const float rb = odd ? Pb.rb : Pa.rb, rc = odd ? Pb.rc : Pa.rc;
+    const uint32_t qpos = odd ? (uint32_t)Pb.qpos : (uint32_t)Pa.qpos;
+    const float t = (px - oa) * inv;
+    const f2v u = __builtin_elementwise_fma(f2v{t, t}, dbc, obc) - f2v{cb, cc};
+    const float ub = fabsf(u.x) - rb, uc = fabsf(u.y) - rc;
+    const float m = __builtin_fmaf(fabsf(t), ma, mb);
+    const bool ok = (fmaxf(ub, uc) <= m) & (t > kPreTmin);
+    const uint32_t key = ok ? ((__float_as_uint(t - m) & ~31u) | qpos) : ~0u;
+    k2 = max(k1, min(k2, key));
+    k1 = min(k1, key);
+  }
+}
+RTP_DEV Hit closest_hit_split(const DevScene* __restrict__ sc, f3 o, f3 d, const float* lds_prex) {
+  const bool odd = (threadIdx.x & 1) != 0;
+  uint64_t key = kNoHitKey;
+  {
+    const int g6 = sc->kind_begin[6], g7 = sc->kind_begin[7], g8 = sc->kind_begin[8], g9 = sc->kind_begin[9],
+              g10 = sc->kind_begin[10], g11 = sc->kind_begin[11];
+    scan_kind_split<7>(sc, g6, g7, o, d, key, odd);
+    scan_kind_split<8>(sc, g7, g8, o, d, key, odd);
+    scan_kind_split<9>(sc, g8, g9, o, d, key, odd);
+    scan_kind_split<10>(sc, g9, g10, o, d, key, odd);
+    scan_kind_split<0>(sc, g10, g11, o, d, key, odd);
+  }
+  const bool lane_ok = (int)(fabsf(o.x) <= kPreLimD) & (int)(fabsf(o.y) <= kPreLimD) & (int)(fabsf(o.z) <= kPreLimD) &
+                       (int)(fabsf(d.x) <= kPreLimD) & (int)(fabsf(d.y) <= kPreLimD) & (int)(fabsf(d.z) <= kPreLimD);
+  const float dmax = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fmaxf(fabsf(d.z), 1.0f));
+  const float omax = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+  const float ma = kPreK * dmax, mb = kPreK * (omax + (sc->pre_scale + 1.0f));
+  uint32_t k1 = ~0u, k2 = ~0u;
+  const int p0 = sc->pre_begin[0], p1 = sc->pre_begin[1], p2 = sc->pre_begin[2], p3 = sc->pre_begin[3];
+  pre_axis_split<0>(sc, p0, p1, o, d, ma, mb, k1, k2, odd);
+  pre_axis_split<1>(sc, p1, p2, o, d, ma, mb, k1, k2, odd);
+  pre_axis_split<2>(sc, p2, p3, o, d, ma, mb, k1, k2, odd);
+  {  // the pair's two smallest keys
+    const uint32_t o1 = pair_swap(k1), o2 = pair_swap(k2);
+    k2 = min(max(k1, o1), min(k2, o2));
+    k1 = min(k1, o1);
+  }
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v* lx = reinterpret_cast<const f4v*>(lds_prex) + 4 * (k1 & 31u);
+  f4v xr[4] = {lx[0], lx[1], lx[2], lx[3]};
+  if (lane_ok && k1 != ~0u) {
+    PreExact Q;
+    __builtin_memcpy(&Q, xr, sizeof(Q));
+    float t;
+    const bool ok = quad_hit_axis(Q, o, d, t);
+    const uint64_t kq = (uint64_t)__float_as_uint(t) << 32 | Q.key_lo;
+    key = (ok && t > 0.001f && kq < key) ? kq : key;
+  }
+  key = pair_min(key);
+  const bool full = !lane_ok || (k2 & ~31u) <= (uint32_t)(key >> 32);
+  if (__ballot(full)) {
+    if (full) {
+      const int g0 = sc->kind_begin[0], g1 = sc->kind_begin[1], g2 = sc->kind_begin[2], g3 = sc->kind_begin[3],
+                g4 = sc->kind_begin[4], g5 = sc->kind_begin[5], g6 = sc->kind_begin[6];
+      scan_kind_split<1>(sc, g0, g1, o, d, key, odd);
+      scan_kind_split<2>(sc, g1, g2, o, d, key, odd);
+      scan_kind_split<3>(sc, g2, g3, o, d, key, odd);
+      scan_kind_split<4>(sc, g3, g4, o, d, key, odd);
+      scan_kind_split<5>(sc, g4, g5, o, d, key, odd);
+      scan_kind_split<6>(sc, g5, g6, o, d, key, odd);
+    }
+    key = pair_min(key);  // (both lanes of a pair take the same branch)
+  }
+  Hit h{3.40282347e+38f, -1, 0};
+  if (key != kNoHitKey) {
+    h.t = __uint_as_float((uint32_t)(key >> 32));
+    h.kind = 0;
+    h.idx = (int)(key & 0xffu);
+  }
+  const int ns = sc->n_spheres;
+  for (int k = 0; k < ns; k++) {
+    const DevSphere& S = sc->spheres[k];
+    float t;
+    if (sphere_hit(o, d, 0.001f, h.t, ld3(S.c), S.rr, t)) {
+      h.t = t;
+      h.kind = 1;
+      h.idx = k;
+    }
+  }
+  return h;
 }
 
 // the two parts of closest_hit (rtp_kernels.hip), each alone
@@ -90,14 +217,16 @@ __global__ void __launch_bounds__(256) lat_kernel(const DevScene* __restrict__ s
   fill_qshade(sc, s_qshade);
   __syncthreads();
   const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  uint32_t seed = 0x9e3779b9u * (blockIdx.x * blockDim.x + threadIdx.x + 1);
+  constexpr bool kSplit = kMode == 8 || kMode == 9 || kMode == 10;  // lane pairs share a ray (identical per-lane state)
+  const int ray = kSplit ? (int)(blockIdx.x * blockDim.x + threadIdx.x) >> 1 : (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  uint32_t seed = 0x9e3779b9u * (ray + 1);
   Path ps;
   ps.org = rand_point(seed);
   ps.dir = rand_dir(seed);
   ps.d = 0;
   ps.nonfinite = false;
   float acc = 0.f;
-  float4* hd = hist + blockIdx.x * blockDim.x + threadIdx.x;
+  float4* hd = hist + ray;
   Hit h0{};
   Path p0 = ps;
   if (kMode == 3) h0 = closest_hit<false>(sc, ps.org, ps.dir, true, nullptr, s_qshade + kPrexLdsOffset);
@@ -116,6 +245,26 @@ __global__ void __launch_bounds__(256) lat_kernel(const DevScene* __restrict__ s
       acc += __uint_as_float((uint32_t)(k >> 32) & 0x3fffffffu);
       ps.org = add(ps.org, scl(ps.dir, 1e-3f * randf(seed)));
       ps.dir = rand_dir(seed);
+    } else if constexpr (kSplit) {
+      const Hit h = closest_hit_split(sc, ps.org, ps.dir, s_qshade + kPrexLdsOffset);
+      if constexpr (kMode == 10) {
+        const Hit w = closest_hit<false>(sc, ps.org, ps.dir, true, nullptr, s_qshade + kPrexLdsOffset);
+        acc += (__float_as_uint(w.t) != __float_as_uint(h.t) || w.kind != h.kind || w.idx != h.idx) ? 1.f : 0.f;
+        ps.org = h.kind >= 0 ? add(ps.org, scl(ps.dir, h.t)) : rand_point(seed);
+        ps.dir = rand_dir(seed);
+      } else if constexpr (kMode == 8) {
+        acc += h.t;
+        ps.org = h.kind >= 0 ? add(ps.org, scl(ps.dir, h.t)) : rand_point(seed);
+        ps.dir = rand_dir(seed);
+      } else {
+        f3 emit;
+        const int r = shade_hit<false, true>(sc, ps, seed, emit, hd, 50, s_qshade, h);
+        if (r != kAlive) {
+          acc += emit.x;
+          ps.org = rand_point(seed);
+          ps.dir = rand_dir(seed);
+        }
+      }
     } else if constexpr (kMode == 3) {
       ps = p0;
       f3 emit;
@@ -170,9 +319,15 @@ void run(const DevScene* sc, int cus, int w, int iters, float4* hist, const uint
   (void)hipMemcpy(c.data(), cyc, c.size() * 8, hipMemcpyDeviceToHost);
   double sum = 0, mx = 0;
   for (auto v : c) sum += (double)v, mx = std::max(mx, (double)v);
-  printf("{\"mode\": %d, \"waves_per_simd\": %d, \"iters\": %d, \"kernel_ms\": %.3f, \"cycles_per_step\": %.1f, "
+  double bad = 0;
+  if (kMode == 10) {
+    std::vector<float> sk((size_t)blocks * 256);
+    (void)hipMemcpy(sk.data(), sink, sk.size() * 4, hipMemcpyDeviceToHost);
+    for (float v : sk) bad += v;
+  }
+  printf("{\"mismatches\": %.0f, \"mode\": %d, \"waves_per_simd\": %d, \"iters\": %d, \"kernel_ms\": %.3f, \"cycles_per_step\": %.1f, "
          "\"max_cycles_per_step\": %.1f, \"ns_per_step_wall\": %.2f, \"wave_steps_per_us\": %.1f}\n",
-         kMode, w, iters, ms, sum / c.size() / iters, mx / iters, ms * 1e6 / iters, (double)c.size() * iters / (ms * 1e3));
+         bad, kMode, w, iters, ms, sum / c.size() / iters, mx / iters, ms * 1e6 / iters, (double)c.size() * iters / (ms * 1e3));
   fflush(stdout);
 }
 }  // namespace lb
@@ -223,6 +378,9 @@ int main(int argc, char** argv) {
         case 5: lb::run<5>(ctx->d_scene, cus, w, iters, hist, tab, cyc, sink); break;
         case 6: lb::run<6>(ctx->d_scene, cus, w, iters, hist, tab, cyc, sink); break;
         case 7: lb::run<7>(ctx->d_scene, cus, w, iters, hist, tab, cyc, sink); break;
+        case 8: lb::run<8>(ctx->d_scene, cus, w, iters, hist, tab, cyc, sink); break;
+        case 9: lb::run<9>(ctx->d_scene, cus, w, iters, hist, tab, cyc, sink); break;
+        case 10: lb::run<10>(ctx->d_scene, cus, w, iters, hist, tab, cyc, sink); break;
         default: break;
       }
     }
