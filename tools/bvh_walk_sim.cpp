@@ -7,7 +7,11 @@
 //   threaded: the 8 octant-ordered threaded copies (bvh_flatten, top-box drop
 //             depth 2 + area ratio 0.6): one box or sphere per visit;
 //   stack:    one copy, children as a pair (both boxes tested per visit, near
-//             child first, far child pushed): visits, max stack depth.
+//             child first, far child pushed): visits, max stack depth;
+//   wide4:    the binary tree collapsed to 4-wide nodes (a node's children are
+//             its binary grandchildren, or children where those are leaves):
+//             every child box tested per visit, hit children visited near to
+//             far through a stack, sphere leaves tested after their box.
 // Prints per-ray means: node visits, box tests, sphere tests, max stack depth,
 // and the layout sizes.  build: g++ -O2 -std=c++17 tools/bvh_walk_sim.cpp
 //   -Iinclude -Lraytracingtherestofyourlife_amd -lrtp -Wl,-rpath,$PWD/raytracingtherestofyourlife_amd
@@ -130,6 +134,15 @@ static bool box_hit(const float* o, const float* inv, const float* lo, const flo
   return t0 <= t1;
 }
 
+// 4-wide collapse: the children of binary node i as up to 4 binary node ids
+static int wide_children(const std::vector<Node>& T, int i, int out[4]) {
+  int n = 0;
+  for (int c : {T[i].left, T[i].right}) {
+    if (T[c].left < 0) out[n++] = c;
+    else out[n++] = T[c].left, out[n++] = T[c].right;
+  }
+  return n;
+}
 struct Stats {
   double visits = 0, boxes = 0, spheres = 0, maxstack = 0, pushes = 0;
   int maxstack_all = 0;
@@ -193,14 +206,22 @@ int main(int argc, char** argv) {
     int depth = 0, leaves = 0, inner = 0;
     for (const Node& n : T) depth = std::max(depth, n.depth), (n.left < 0 ? leaves : inner)++;
     // threaded walk = depth-first near-first traversal with box culling at every node (top drop ignored)
-    Stats th, sk;
+    Stats th, th_oracle, sk, wd;
     for (int r = 0; r < nrays; r++) {
       const float* o = &rays[6 * r];
       const float* dd = o + 3;
       const float inv[3] = {1.f / dd[0], 1.f / dd[1], 1.f / dd[2]};
-      // threaded: visit node; if box hit (or leaf) continue into it
-      {
-        float best = wall_t(o, dd);
+      // threaded: visit node; if box hit (or leaf) continue into it (pass 0:
+      // bounded by the walls; pass 1: by the true closest hit, the bound a
+      // perfect first guess would give -- how many visits culling could save)
+      float t_true = wall_t(o, dd);
+      for (const Sph& s2 : S) {
+        float t;
+        if (sphere_t(o, dd, s2, t) && t < t_true) t_true = t;
+      }
+      for (int pass = 0; pass < 2; pass++) {
+        Stats& acc = pass ? th_oracle : th;
+        float best = pass ? t_true * 1.00001f : wall_t(o, dd);
         int visits = 0, spheres = 0;
         std::vector<int> stk{0};
         while (!stk.empty()) {
@@ -228,8 +249,8 @@ int main(int argc, char** argv) {
           stk.push_back(neg ? n.left : n.right);
           stk.push_back(neg ? n.right : n.left);
         }
-        th.visits += visits;
-        th.spheres += spheres;
+        acc.visits += visits;
+        acc.spheres += spheres;
       }
       // stack walk over child pairs
       {
@@ -293,6 +314,43 @@ int main(int argc, char** argv) {
         sk.pushes += pushes;
         sk.maxstack_all = std::max(sk.maxstack_all, maxs);
       }
+      // 4-wide walk
+      {
+        float best = wall_t(o, dd);
+        int visits = 0, spheres = 0, boxes = 0, maxs = 0;
+        std::vector<std::pair<int, float>> stk{{0, 0.f}};
+        while (!stk.empty()) {
+          auto e = stk.back();
+          stk.pop_back();
+          if (e.second > best) continue;
+          const Node& n = T[e.first];
+          if (n.left < 0) {  // a leaf (root only, or pushed leaf)
+            for (int j = 0; j < n.count; j++) {
+              float t;
+              spheres++;
+              if (sphere_t(o, dd, S[order[n.first + j]], t) && t < best) best = t;
+            }
+            continue;
+          }
+          visits++;
+          int ch[4];
+          const int nc = wide_children(T, e.first, ch);
+          std::vector<std::pair<float, int>> hits;
+          for (int k = 0; k < nc; k++) {
+            float tn;
+            boxes++;
+            if (box_hit(o, inv, T[ch[k]].lo, T[ch[k]].hi, best, tn)) hits.push_back({tn, ch[k]});
+          }
+          std::sort(hits.begin(), hits.end());
+          for (int k = (int)hits.size() - 1; k >= 0; k--) stk.push_back({hits[k].second, hits[k].first});
+          maxs = std::max(maxs, (int)stk.size());
+        }
+        wd.visits += visits;
+        wd.spheres += spheres;
+        wd.boxes += boxes;
+        wd.maxstack += maxs;
+        wd.maxstack_all = std::max(wd.maxstack_all, maxs);
+      }
     }
     const double n = nrays;
     printf("leaf<=%d: %d nodes (%d inner, %d leaves), depth %d | threaded: %.1f visits %.1f sphere tests per ray, "
@@ -301,6 +359,12 @@ int main(int argc, char** argv) {
            leaf, (int)T.size(), inner, leaves, depth, th.visits / n, th.spheres / n, 8.0 * T.size() * 16 / 1024,
            sk.visits / n, sk.boxes / n, sk.spheres / n, sk.pushes / n, sk.maxstack / n, sk.maxstack_all,
            inner * 32.0 / 1024);
+    printf("   threaded with the true hit as the initial bound: %.1f visits %.1f sphere tests per ray\n",
+           th_oracle.visits / n, th_oracle.spheres / n);
+    printf("   wide4: %.1f node visits %.1f box tests %.1f sphere tests per ray, max stack mean %.1f / worst %d; "
+           "gathers per ray: threaded %.1f x 16 B = %.0f B, wide4 (48-B quantized nodes + 16-B spheres) %.1f x 16 B = %.0f B\n",
+           wd.visits / n, wd.boxes / n, wd.spheres / n, wd.maxstack / n, wd.maxstack_all, th.visits / n,
+           16 * th.visits / n, (3 * wd.visits + wd.spheres) / n, 16 * (3 * wd.visits + wd.spheres) / n);
   }
   return 0;
 }
