@@ -629,6 +629,7 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     return t >= 0 && t < s->n_tex_type && s->tex_type[t] >= 0 && s->tex_type[t] < s->n_tex;
   };
   rtp::DevScene* h = new rtp::DevScene();
+  h->oct_mask = 7;  // (every octant its own walk order; the host SAH build may narrow it)
   std::memset(h, 0, sizeof(*h));
   std::vector<int> kept;
   std::vector<rtp::DevQuad> built;
@@ -767,10 +768,15 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     float drop_sa = kBvhDropArea;
     if (const char* dd = getenv("RTP_BVH_DROP")) drop = std::max(0, std::min(16, atoi(dd)));
     if (const char* da = getenv("RTP_BVH_DROP_SA")) drop_sa = (float)atof(da);
+    // the copies the walk reads: octant o walks copy (o & oct_mask)
+    // (RTP_BVH_OCT_MASK; the other copies are built the same and never read)
+    int oct_mask = 7;
+    if (const char* om = getenv("RTP_BVH_OCT_MASK")) oct_mask = atoi(om) & 7;
+    h->oct_mask = oct_mask;
     int per_oct = 0;
     for (int oct = 0; oct < 8; oct++) {  // 8 copies of n_nodes entries, indices local to each copy
       std::vector<rtp::BvhNode> one;
-      bvh_flatten(tree, 0, oct, order, sph, one, 0, drop, drop_sa);
+      bvh_flatten(tree, 0, oct & oct_mask, order, sph, one, 0, drop, drop_sa);
       per_oct = (int)one.size();  // (the same nodes are dropped in every octant's order)
       nodes.insert(nodes.end(), one.begin(), one.end());
     }

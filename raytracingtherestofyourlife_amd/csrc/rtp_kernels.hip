@@ -168,7 +168,7 @@ RTP_DEV int ray_octant(f3 d) { return (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) 
 // kLds: the LDS walk's tree (its global side tables; the nodes are read from LDS)
 template <bool kLds = false>
 RTP_DEV BvhRay bvh_ray(const DevScene* __restrict__ sc, f3 o, f3 d) {
-  const int oct = ray_octant(d);
+  const int oct = ray_octant(d) & (kLds ? 7 : sc->oct_mask);
   const int64_t base = (int64_t)oct * (kLds ? sc->n_lw_nodes : sc->n_nodes);
   BvhRay R;
   R.nodes = (GU4*)((kLds ? sc->lw_nodes : sc->cnodes) + 4 * base);
@@ -1282,7 +1282,14 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
         // the LDS walk: this octant's copy of the nodes, then the leaf spheres
         LU4* const lnodes = (LU4*)s_bvh + (kLdsBvh ? ray_octant(d) * nn : 0);
         LF4* const lsph = (LF4*)s_bvh + (kLdsBvh ? 8 * nn : 0);
-        auto node = [&](int i) { return kLdsBvh ? lnodes[i] : R.nodes[i]; };
+#ifndef RTP_BVH_NT
+#define RTP_BVH_NT 0  // (experiment: the walk's node gathers as non-temporal loads)
+#endif
+        auto node = [&](int i) {
+          if constexpr (kLdsBvh) return lnodes[i];
+          else if constexpr (RTP_BVH_NT) return __builtin_nontemporal_load(R.nodes + i);
+          else return R.nodes[i];
+        };
         u4v v = u4v{0u, 0u, 0u, 0u};
         if (walking) v = node(wni);
         for (;;) {

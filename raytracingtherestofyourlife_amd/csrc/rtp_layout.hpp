@@ -219,7 +219,11 @@ struct alignas(16) DevScene {
   const float* lw_sph;       // n_lw_sph float4s (centre, r^2) in the leaf order of lw_nodes
   const int32_t* lw_orig;    // n_lw_sph: the scene index of each
   int32_t n_lw_sph;
-  int32_t pad3[3];
+  // the global walk's copies: a ray in octant o walks copy (o & oct_mask);
+  // bits left out of the mask order those axes' splits left child first
+  // (fewer distinct copies: a smaller footprint in the texture cache)
+  int32_t oct_mask;
+  int32_t pad3[2];
 };
 // The pool kernel's scans prefetch up to two records past the last quad or
 // prefilter record; these must stay inside DevScene (values never used).

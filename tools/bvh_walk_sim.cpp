@@ -207,6 +207,7 @@ int main(int argc, char** argv) {
     for (const Node& n : T) depth = std::max(depth, n.depth), (n.left < 0 ? leaves : inner)++;
     // threaded walk = depth-first near-first traversal with box culling at every node (top drop ignored)
     Stats th, th_oracle, sk, wd;
+    std::vector<double> depth_visits(32, 0.0);
     for (int r = 0; r < nrays; r++) {
       const float* o = &rays[6 * r];
       const float* dd = o + 3;
@@ -229,6 +230,7 @@ int main(int argc, char** argv) {
           stk.pop_back();
           const Node& n = T[i];
           visits++;
+          if (pass == 0) depth_visits[std::min(n.depth, 31)]++;
           if (n.left < 0 && n.count == 1) {  // embedded sphere: exact test, no box
             float t;
             spheres++;
@@ -359,6 +361,55 @@ int main(int argc, char** argv) {
            leaf, (int)T.size(), inner, leaves, depth, th.visits / n, th.spheres / n, 8.0 * T.size() * 16 / 1024,
            sk.visits / n, sk.boxes / n, sk.spheres / n, sk.pushes / n, sk.maxstack / n, sk.maxstack_all,
            inner * 32.0 / 1024);
+    {
+      double tot = 0, cum = 0;
+      for (double v : depth_visits) tot += v;
+      printf("   threaded visits by node depth (cumulative share; nodes at depth <= k per octant copy):");
+      int nodes_le = 0;
+      for (int k = 0; k < 14; k++) {
+        cum += depth_visits[k];
+        for (const Node& nd : T) nodes_le += nd.depth == k;
+        printf(" %d:%.2f/%d", k, cum / tot, nodes_le);
+      }
+      printf("\n");
+    }
+    // fewer octant copies: near-first only at nodes split along a covered
+    // axis (mask bit k: axis k's sign picks the copy), left child first elsewhere
+    for (int cover : {7, 5, 1, 2, 4, 0}) {
+      double v = 0;
+      for (int r2 = 0; r2 < nrays; r2++) {
+        const float* o2 = &rays[6 * r2];
+        const float* d2 = o2 + 3;
+        const float inv2[3] = {1.f / d2[0], 1.f / d2[1], 1.f / d2[2]};
+        float best = wall_t(o2, d2);
+        std::vector<int> stk{0};
+        while (!stk.empty()) {
+          const int i = stk.back();
+          stk.pop_back();
+          const Node& nd = T[i];
+          v++;
+          if (nd.left < 0 && nd.count == 1) {
+            float t;
+            if (sphere_t(o2, d2, S[order[nd.first]], t) && t < best) best = t;
+            continue;
+          }
+          float tn;
+          if (!box_hit(o2, inv2, nd.lo, nd.hi, best, tn)) continue;
+          if (nd.left < 0) {
+            for (int j = 0; j < nd.count; j++) {
+              float t;
+              if (sphere_t(o2, d2, S[order[nd.first + j]], t) && t < best) best = t;
+            }
+            continue;
+          }
+          const bool neg = ((cover >> nd.axis) & 1) && d2[nd.axis] < 0;
+          stk.push_back(neg ? nd.left : nd.right);
+          stk.push_back(neg ? nd.right : nd.left);
+        }
+      }
+      printf("   threaded, copies for axes mask %d (%d copies): %.1f visits per ray\n", cover,
+             1 << __builtin_popcount(cover), v / nrays);
+    }
     printf("   threaded with the true hit as the initial bound: %.1f visits %.1f sphere tests per ray\n",
            th_oracle.visits / n, th_oracle.spheres / n);
     printf("   wide4: %.1f node visits %.1f box tests %.1f sphere tests per ray, max stack mean %.1f / worst %d; "
