@@ -29,8 +29,15 @@ def hipcc() -> str:
 
 
 def flags() -> list[str]:
+    # -fno-slp-vectorize: the SLP vectorizer paired scalar float products
+    # (dot products, cross products) into v_pk_mul_f32 / v_pk_add_f32, each
+    # followed by an s_nop before its result is read (gfx950's packed-FP32
+    # hazard); scalar they need none.  C2 101.5-102.9 -> 96.2-97.2 ms (-5.5%),
+    # C3 -3.2% (profiles/r04n_ab_noslp.txt).  The explicit packed pairs of the
+    # quad tests (ext_vector_type) stay packed.  Results are the same bits:
+    # a packed half rounds like the scalar instruction.
     return ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-            "-fno-fast-math", "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+            "-fno-fast-math", "-fno-slp-vectorize", "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
 
 
 def stale() -> bool:

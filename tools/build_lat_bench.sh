@@ -4,7 +4,7 @@
 set -e
 cd "$(dirname "$0")/.."
 out=tools/lat_bench${1:+_$1}; shift || true
-/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off -fno-fast-math "$@" \
+/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off -fno-fast-math -fno-slp-vectorize "$@" \
   -I raytracingtherestofyourlife_amd/csrc tools/lat_bench.hip -L raytracingtherestofyourlife_amd -lrtp \
   -Wl,-rpath,'$ORIGIN/../raytracingtherestofyourlife_amd' -o "$out"
 echo "$out"

@@ -13,7 +13,7 @@ if [ -n "$RTP_SRC_REV" ]; then
   src=$tmp/raytracingtherestofyourlife_amd/csrc
 fi
 mkdir -p "$(dirname "$out")"
-/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math "$@" \
+/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math -fno-slp-vectorize "$@" \
   -o "$out" "$src"/rtp_kernels.hip "$src"/rtp_direct.hip "$src"/rtp_bvh_gpu.hip "$src"/rtp_host.cpp \
   "$src"/rtp_direct_host.cpp "$src"/scene_cornell.cpp
 [ -n "$RTP_SRC_REV" ] && rm -rf "$tmp"

@@ -23,7 +23,7 @@ CSRC = os.path.join(ROOT, "raytracingtherestofyourlife_amd", "csrc")
 
 
 def compile_asm(out: str, defines: list[str]) -> None:
-    cmd = ["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+    cmd = ["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fno-slp-vectorize",
            "--cuda-device-only", "-S", "-gline-tables-only", *defines, "-o", out,
            os.path.join(CSRC, "rtp_kernels.hip"), f"-I{CSRC}"]
     subprocess.run(cmd, check=True, capture_output=True)
