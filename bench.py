@@ -2,7 +2,10 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload auto|c2|c4] [--scaling strong|weak]
 
-One step = one full render of the workload's frame.
+One step = one full render of the workload's frame.  On one GPU (no process
+group) the frame goes through the library's default contiguous launch
+(rtp_render_device over [0, nx*ny), like main.cc's render; --n1-launch tiles:
+the tile-deal instance the ranks of an N-GPU run use).
   c2: Cornell Box 800x800, 1000 spp, depth 50 (BASELINE.json configs[1]), the
       metric's own image: the N = 1 workload (--workload auto).
   c4: Cornell Box 1920x1080, 4096 spp, depth 50 (BASELINE.json configs[3]),
@@ -198,6 +201,10 @@ def main() -> None:
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c2.json"))
     ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "valu_c2.json"))
     ap.add_argument("--golden", default=None, help="whole-frame fixture (c2) or pixel-subset fixture (c4)")
+    ap.add_argument("--n1-launch", default="contig", choices=["contig", "tiles"],
+                    help="one GPU, no process group: contig = the whole frame through the library's default launch "
+                         "(rtp_render_device over [0, nx*ny), like main.cc's render); tiles = the tile-deal instance "
+                         "the ranks of an N-GPU run use (rank 0 of 1)")
     args = ap.parse_args()
 
     import torch
@@ -229,7 +236,11 @@ def main() -> None:
 
     strong = args.scaling == "strong"
     nx, ny = args.nx, args.ny * (1 if strong else world)
-    ids_np = shard.tile_pixels(nx, ny, rank, world)
+    # one GPU without a process group renders the frame in pixel order through
+    # the default contiguous launch (--n1-launch contig); ranks of a group
+    # render their tiles
+    contig = world == 1 and not (args.force_collective) and args.n1_launch == "contig"
+    ids_np = np.arange(nx * ny, dtype=np.int64) if contig else shard.tile_pixels(nx, ny, rank, world)
     npix = ids_np.size
     # setup, timed: the context, the scene, the RNG jump tables (policy), then
     # the first render -- what a fresh process pays before its first frame.
@@ -265,10 +276,13 @@ def main() -> None:
 
     # the rank's tiles: computed in the kernel (rtp_render_tiles_device) when
     # the canvas is whole tiles, else the explicit pixel list
-    tiled = nx % TILE == 0 and ny % TILE == 0 and os.environ.get("RTP_BENCH_LIST") != "1"
+    tiled = (not contig) and nx % TILE == 0 and ny % TILE == 0 and os.environ.get("RTP_BENCH_LIST") != "1"
 
     def render():
-        if tiled:
+        if contig:
+            dev.render_device(cam, nx, ny, args.spp, args.depth, out.data_ptr(), pixel_count=npix,
+                              stream=stream.cuda_stream)
+        elif tiled:
             dev.render_tiles_device(cam, nx, ny, args.spp, args.depth, out.data_ptr(), rank, world,
                                     stream=stream.cuda_stream)
         else:
@@ -278,7 +292,8 @@ def main() -> None:
     def step(count_live: bool = False):
         if count_live:  # (the list path carries the per-pixel live-bounce counters)
             dev.render_device(cam, nx, ny, args.spp, args.depth, out.data_ptr(), pixel_count=npix,
-                              pixel_ids_ptr=ids.data_ptr(), stream=stream.cuda_stream, live_ptr=live.data_ptr())
+                              pixel_ids_ptr=0 if contig else ids.data_ptr(), stream=stream.cuda_stream,
+                              live_ptr=live.data_ptr())
         else:
             render()
         return gather_canvas()
@@ -323,16 +338,22 @@ def main() -> None:
         check = bool(same.all())
     # a one-shot render on the library's default policy (AUTO: no jump tables
     # for a single C2 frame), as main.cc's rtp_render would run it: the whole
-    # frame, contiguous pixels, tables switched off (one process: N = 1 only;
-    # a different kernel instance from the timed tile deal, so the rocprof
-    # statistics of the timed instance stay the timed renders')
+    # frame, tables switched off (one process: N = 1 only).  It runs through
+    # the OTHER kernel instance than the timed renders (the tile deal when the
+    # timed launch is contiguous, the contiguous launch when it is the tile
+    # deal; the two render at rates within ~1%, r04q), so the rocprof
+    # statistics of the timed instance stay the timed renders'.
     off_ms = float("nan")
     if world == 1:
         dev.set_ff_tables("off")
         full_off = torch.empty((nx * ny, 4), dtype=torch.float32, device="cuda")
         torch.cuda.synchronize()
         t_off = time.perf_counter()
-        dev.render_device(cam, nx, ny, args.spp, args.depth, full_off.data_ptr(), stream=stream.cuda_stream)
+        if contig and nx % TILE == 0 and ny % TILE == 0:
+            dev.render_tiles_device(cam, nx, ny, args.spp, args.depth, full_off.data_ptr(), 0, 1,
+                                    stream=stream.cuda_stream)
+        else:
+            dev.render_device(cam, nx, ny, args.spp, args.depth, full_off.data_ptr(), stream=stream.cuda_stream)
         torch.cuda.synchronize()
         off_ms = (time.perf_counter() - t_off) * 1e3
         del full_off
@@ -382,7 +403,9 @@ def main() -> None:
             cpu = cpu_baseline(args.cpu_budget, args.nx, args.ny, args.depth)
         if world == 1 and args.cpu_budget_mt > 0:
             cpu_mt = cpu_baseline(args.cpu_budget_mt, args.nx, args.ny, args.depth, nthreads=host_threads())
-        if world == 1 and not grouped:
+        if contig:
+            shard_desc = "one GPU: the whole frame in pixel order (the default contiguous launch)"
+        elif world == 1 and not grouped:
             shard_desc = "one GPU: the whole frame"
         else:
             shard_desc = (f"{TILE}x{TILE} tiles round-robin over {world} rank(s), 1 "
@@ -405,7 +428,8 @@ def main() -> None:
                 "workload": W["name"] + ("" if strong or world == 1 else f" per GPU (canvas {nx}x{ny})"),
                 "nx": nx, "ny": ny, "spp": args.spp, "depth": args.depth,
                 "pixels_per_gpu": npix,
-                "shard": shard_desc + (" (pixel of each tile entry computed in-kernel)" if tiled else " (pixel list)"),
+                "shard": shard_desc + ("" if contig else " (pixel of each tile entry computed in-kernel)" if tiled
+                                       else " (pixel list)"),
                 "live_bounces_per_sample": round(L, 6),
                 "dist_backend": args.dist_backend if grouped else None,
             },
@@ -417,7 +441,8 @@ def main() -> None:
             "one_shot": None if world > 1 else {
                 "note": "a fresh process rendering this frame once, like main.cc (its timer, :584-585, 661-663; "
                         "process start, imports and the HIP runtime's first-use initialisation excluded): "
-                        "context + scene + jump-table policy + one render",
+                        "context + scene + jump-table policy + one render (its render through the other kernel "
+                        "instance than the timed one: within ~1%)",
                 "default_policy": {"policy": "auto (no tables for one frame)",
                                    "end_to_end_ms": round(setup_base_ms + off_ms, 1),
                                    "render_ms": round(off_ms, 1),
