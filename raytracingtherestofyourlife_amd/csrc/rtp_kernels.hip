@@ -1447,7 +1447,7 @@ __global__ void __launch_bounds__(64 * kLdsBvhWavesPerBlock, 1) __attribute__((a
 constexpr int kLdsWalkStaticBytes =
     kLdsBvhWavesPerBlock * kPool * kSlotBytes + kQTableFloats * 4 + kLdsBvhWavesPerBlock * kPool * 4;
 constexpr int kLdsWalkDynBytes = 160 * 1024 - kLdsWalkStaticBytes;  // the tree's share of the CU's 160 KiB
-static_assert(kLdsWalkDynBytes >= 64 * 1024, "the LDS walk keeps room for a C3-size tree");
+static_assert(kPool != 128 || kLdsWalkDynBytes >= 64 * 1024, "the LDS walk keeps room for a C3-size tree");
 
 // ------------------------------------------------------- diagnostics ---
 __global__ void rtp_eval_primitive_kernel(int kind, const void* in, void* out, int64_t n, const uint32_t* tab,
@@ -1716,7 +1716,7 @@ extern "C" int rtp_plan_steal(int64_t npix, int bvh) {
 
 // Bytes of LDS the LDS walk's tree may take (nodes of 8 octant copies plus
 // the leaf spheres, 16 B each): what the 16-wave block leaves of the CU's 160 KiB.
-extern "C" int rtp_lds_walk_capacity(void) { return rtp::kLdsWalkDynBytes; }
+extern "C" int rtp_lds_walk_capacity(void) { return std::max(0, rtp::kLdsWalkDynBytes); }
 
 extern "C" hipError_t rtp_launch_eval_closest(const rtp::DevScene* scene, const float* rays, uint32_t* out,
                                               int64_t n, int bvh, hipStream_t stream) {
