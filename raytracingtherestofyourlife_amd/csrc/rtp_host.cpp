@@ -24,7 +24,6 @@
 
 extern "C" int64_t rtp_plan_history_lanes(int64_t npix, int spp, int bvh, int* variant_out, int* waves_out);
 extern "C" int rtp_plan_steal(int64_t npix, int bvh);
-extern "C" int rtp_pair_resident_waves(void);
 extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::KParams* p, int variant, int waves, int bvh,
                                         hipStream_t stream, int lds_bytes);
 extern "C" int rtp_lds_walk_capacity(void);
@@ -1047,20 +1046,6 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
       lanes = (int64_t)sw * 128;
     }
   }
-  // two paths per lane for a launch whose 128-pixel waves all fit at once
-  // (opt-in RTP_PAIR=1: rtp_render_pool_pair, a short share's idle issue
-  // slots spent on a second path per lane)
-  if (variant == 2 && !d_wave_begin && !stats_on && bvh == 0 && spp > 0) {
-    const char* pe = getenv("RTP_PAIR");
-    if (pe && pe[0] == '1') {
-      const int64_t pw = (npix + 128 - 1) / 128;
-      if (pw <= rtp_pair_resident_waves()) {
-        variant = 3;
-        waves = (int)pw;
-        lanes = pw * 128;
-      }
-    }
-  }
   // D rows per lane (row k of a light hit holds E_k), rounded up to 8 (a
   // slot-major history pads each slot to whole 128-byte lines)
   size_t hist_need = (size_t)((depth + 7) & ~7) * (size_t)lanes * 16;
@@ -1069,7 +1054,7 @@ rtp_status launch(rtp_context* c, const rtp_camera* cam, int32_t nx, int32_t ny,
   p.hist = c->d_hist;
   p.dbg = nullptr;
   p.progress = c->d_progress;
-  if (variant >= 2) {
+  if (variant == 2) {
     const FfSnap ft = ff_tables(c->device, c->ff_policy, (uint64_t)npix * (uint64_t)spp);
     for (int j = 0; j < rtp::kFfTables; j++) p.ff[j] = ft.t[j];
     p.ffd = ft.direct, p.ffd_first = ft.d_first, p.ffd_count = ft.d_count;

@@ -512,174 +512,6 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
   return h;
 }
 
-// ---- two paths per lane (rtp_render_pool_pair, tools/lat_bench modes 11-13) ----
-// closest_hit<false> for rays A and B together: every scalar-loaded quad head
-// and prefilter record is tested against both rays, so the two rays'
-// dependent chains interleave (ILP in place of a second wave on a SIMD that a
-// short launch leaves half empty).  Same keys, same minimum: bit-identical to
-// two closest_hit calls (tools/lat_bench mode 13).  act_a / act_b: the lane
-// carries that path (an idle ray never forces the exact scan).
-template <int K>
-RTP_DEV void scan_kind_pf2(const DevScene* __restrict__ sc, int b, int e, f3 oa, f3 da, uint64_t& ba, f3 ob, f3 db,
-                           uint64_t& bb, u16v& cur) {
-  const DevQuad* qp = sc->quads + b;
-  for (int n = e - b; n > 0; n -= 2, qp += 2) {
-    const u16v nxt = head_at(qp + 1);
-    scan_one<K>(qp[0], cur, oa, da, ba);
-    scan_one<K>(qp[0], cur, ob, db, bb);
-    if (n == 1) {
-      cur = nxt;
-      break;
-    }
-    cur = head_at(qp + 2);
-    scan_one<K>(qp[1], nxt, oa, da, ba);
-    scan_one<K>(qp[1], nxt, ob, db, bb);
-  }
-}
-struct PreRay {
-  float inv, oa, ma, mb;
-  f2v obc, dbc;
-  uint32_t k1, k2;
-};
-template <int A>
-RTP_DEV void pre_setup(PreRay& r, f3 o, f3 d) {
-  constexpr int B = (A + 1) % 3, C = (A + 2) % 3;
-  r.inv = __builtin_amdgcn_rcpf(comp<A>(d));
-  r.oa = comp<A>(o);
-  r.obc = f2v{comp<B>(o), comp<C>(o)};
-  r.dbc = f2v{comp<B>(d), comp<C>(d)};
-}
-RTP_DEV void pre_fold(PreRay& r, const PreQuad& P) {
-  const float t = (P.x - r.oa) * r.inv;
-  const f2v u = __builtin_elementwise_fma(f2v{t, t}, r.dbc, r.obc) - f2v{P.cb, P.cc};
-  const float ub = fabsf(u.x) - P.rb, uc = fabsf(u.y) - P.rc;
-  const float m = __builtin_fmaf(fabsf(t), r.ma, r.mb);
-  const bool ok = (fmaxf(ub, uc) <= m) & (t > kPreTmin);
-  uint32_t key;
-  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(key) : "v"(__float_as_uint(t - m)), "v"(~31u), "s"((uint32_t)P.qpos));
-  key = ok ? key : ~0u;
-  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r.k2) : "v"(r.k1), "v"(r.k2), "v"(key));
-  r.k1 = min(r.k1, key);
-}
-template <int A>
-RTP_DEV void pre_axis2(const DevScene* __restrict__ sc, int b, int e, f3 oa, f3 da, PreRay& ra, f3 ob, f3 db, PreRay& rb,
-                       u8v& cur) {
-  if (b == e) return;
-  pre_setup<A>(ra, oa, da);
-  pre_setup<A>(rb, ob, db);
-  auto as_pre = [](const u8v& v) {
-    PreQuad P;
-    __builtin_memcpy(&P, &v, sizeof(P));
-    return P;
-  };
-  const PreQuad* pq = sc->pre + b;
-  for (int n = e - b; n > 0; n -= 2, pq += 2) {
-    const u8v nxt = *reinterpret_cast<const u8v*>(pq + 1);
-    const PreQuad P0 = as_pre(cur);
-    pre_fold(ra, P0);
-    pre_fold(rb, P0);
-    if (n == 1) {
-      cur = nxt;
-      break;
-    }
-    cur = *reinterpret_cast<const u8v*>(pq + 2);
-    const PreQuad P1 = as_pre(nxt);
-    pre_fold(ra, P1);
-    pre_fold(rb, P1);
-  }
-}
-RTP_DEV void pre_candidate(f3 o, f3 d, const PreRay& r, bool lane_ok, const float* lds_prex, uint64_t& key) {
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  const f4v* lx = reinterpret_cast<const f4v*>(lds_prex) + 4 * (r.k1 & 31u);
-  f4v xr[4] = {lx[0], lx[1], lx[2], lx[3]};
-  if (lane_ok && r.k1 != ~0u) {
-    PreExact Q;
-    __builtin_memcpy(&Q, xr, sizeof(Q));
-    float t;
-    const bool ok = quad_hit_axis(Q, o, d, t);
-    const uint64_t kq = (uint64_t)__float_as_uint(t) << 32 | Q.key_lo;
-    key = (ok && t > 0.001f && kq < key) ? kq : key;
-  }
-}
-RTP_DEV bool pre_lane_ok(f3 o, f3 d) {
-  return (int)(fabsf(o.x) <= kPreLimD) & (int)(fabsf(o.y) <= kPreLimD) & (int)(fabsf(o.z) <= kPreLimD) &
-         (int)(fabsf(d.x) <= kPreLimD) & (int)(fabsf(d.y) <= kPreLimD) & (int)(fabsf(d.z) <= kPreLimD);
-}
-RTP_DEV void pre_margins(const DevScene* __restrict__ sc, f3 o, f3 d, PreRay& r) {
-  const float dmax = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fmaxf(fabsf(d.z), 1.0f));
-  const float omax = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
-  r.ma = kPreK * dmax;
-  r.mb = kPreK * (omax + (sc->pre_scale + 1.0f));
-  r.k1 = ~0u;
-  r.k2 = ~0u;
-}
-RTP_DEV Hit key_hit(const DevScene* __restrict__ sc, uint64_t key, f3 o, f3 d) {
-  Hit h{3.40282347e+38f, -1, 0};
-  if (key != kNoHitKey) {
-    h.t = __uint_as_float((uint32_t)(key >> 32));
-    h.kind = 0;
-    h.idx = (int)(key & 0xffu);
-  }
-  const int ns = sc->n_spheres;
-  for (int k = 0; k < ns; k++) {
-    const DevSphere& S = sc->spheres[k];
-    float t;
-    if (sphere_hit(o, d, 0.001f, h.t, ld3(S.c), S.rr, t)) {
-      h.t = t;
-      h.kind = 1;
-      h.idx = k;
-    }
-  }
-  return h;
-}
-RTP_DEV void closest_hit2(const DevScene* __restrict__ sc, f3 oa, f3 da, Hit& ha, bool act_a, f3 ob, f3 db, Hit& hb,
-                          bool act_b, const float* lds_prex) {
-  uint64_t ka = kNoHitKey, kb = kNoHitKey;
-  {
-    const int g6 = sc->kind_begin[6], g7 = sc->kind_begin[7], g8 = sc->kind_begin[8], g9 = sc->kind_begin[9],
-              g10 = sc->kind_begin[10], g11 = sc->kind_begin[11];
-    u16v cur = quad_head(sc, g6);
-    scan_kind_pf2<7>(sc, g6, g7, oa, da, ka, ob, db, kb, cur);
-    scan_kind_pf2<8>(sc, g7, g8, oa, da, ka, ob, db, kb, cur);
-    scan_kind_pf2<9>(sc, g8, g9, oa, da, ka, ob, db, kb, cur);
-    scan_kind_pf2<10>(sc, g9, g10, oa, da, ka, ob, db, kb, cur);
-    scan_kind_pf2<0>(sc, g10, g11, oa, da, ka, ob, db, kb, cur);
-  }
-  bool fa = true, fb = true;  // the lane needs the exact scan of the axis-plane quads for ray A / B
-  if (sc->n_pre > 0) {          // (wave-uniform)
-    const bool oka = pre_lane_ok(oa, da), okb = pre_lane_ok(ob, db);
-    PreRay ra, rb;
-    pre_margins(sc, oa, da, ra);
-    pre_margins(sc, ob, db, rb);
-    const int p0 = sc->pre_begin[0], p1 = sc->pre_begin[1], p2 = sc->pre_begin[2], p3 = sc->pre_begin[3];
-    u8v pcur = pre_rec(sc, p0);
-    pre_axis2<0>(sc, p0, p1, oa, da, ra, ob, db, rb, pcur);
-    pre_axis2<1>(sc, p1, p2, oa, da, ra, ob, db, rb, pcur);
-    pre_axis2<2>(sc, p2, p3, oa, da, ra, ob, db, rb, pcur);
-    pre_candidate(oa, da, ra, oka, lds_prex, ka);
-    pre_candidate(ob, db, rb, okb, lds_prex, kb);
-    fa = !oka || (ra.k2 & ~31u) <= (uint32_t)(ka >> 32);
-    fb = !okb || (rb.k2 & ~31u) <= (uint32_t)(kb >> 32);
-  }
-  fa = fa && act_a;
-  fb = fb && act_b;
-  if (__ballot(fa | fb)) {
-    if (fa | fb) {  // the exact scan for both rays (a full scan's minimum is the exact one either way)
-      const int g0 = sc->kind_begin[0], g1 = sc->kind_begin[1], g2 = sc->kind_begin[2], g3 = sc->kind_begin[3],
-                g4 = sc->kind_begin[4], g5 = sc->kind_begin[5], g6 = sc->kind_begin[6];
-      u16v cur = quad_head(sc, g0);
-      scan_kind_pf2<1>(sc, g0, g1, oa, da, ka, ob, db, kb, cur);
-      scan_kind_pf2<2>(sc, g1, g2, oa, da, ka, ob, db, kb, cur);
-      scan_kind_pf2<3>(sc, g2, g3, oa, da, ka, ob, db, kb, cur);
-      scan_kind_pf2<4>(sc, g3, g4, oa, da, ka, ob, db, kb, cur);
-      scan_kind_pf2<5>(sc, g4, g5, oa, da, ka, ob, db, kb, cur);
-      scan_kind_pf2<6>(sc, g5, g6, oa, da, ka, ob, db, kb, cur);
-    }
-  }
-  ha = key_hit(sc, ka, oa, da);
-  hb = key_hit(sc, kb, ob, db);
-}
-
 // Camera::RayGen (Camera.cxx:482-524): 2 draws, jittered direction
 template <class Cam>  // DevCamera, or one read through an address-space-4 (kernarg) reference
 RTP_DEV f3 camera_ray(const Cam& cam, int pi, int pj, int nx, int ny, uint32_t& seed) {
@@ -1594,274 +1426,6 @@ __global__ void __launch_bounds__(256, RTP_POOL_MIN_WAVES_PER_EU) RTP_POOL_VGPR_
   }
 }
 
-// ---- two paths per lane: short launches (opt-in RTP_PAIR=1) ----
-// A launch with fewer pixels than the chip has lanes at five waves per SIMD
-// (a rank's share of a multi-GPU frame) leaves one or two waves per SIMD,
-// and each bounce step then runs at nearly a lone wave's latency (DESIGN.md
-// §4.1 latency table, §6).  Here each lane carries TWO paths of its wave's
-// 128-pixel pool (virtual lanes v = lane and 64 + lane): one closest-hit
-// pass tests every scalar-loaded quad against both rays (closest_hit2), so
-// the two dependent chains interleave in one instruction stream.  The pool
-// protocol is pool_body's (same queues, same fast-forward batch, same
-// sample order per pixel), so results are bit-identical; no sphere BVH, no
-// plan, no stealing, no stats (the host picks this kernel only then).
-template <bool kTiles>
-__device__ __forceinline__ void pool_body_pair(const DevScene* __restrict__ sc, const KParams& p, int n_waves,
-                                               unsigned char* smem, float* s_qshade) {
-  const int lane = threadIdx.x & 63;
-  const int wib = threadIdx.x >> 6;
-  const int w = blockIdx.x * kWavesPerBlock + wib;
-  fill_qshade(sc, s_qshade);
-  __syncthreads();
-  if (w >= n_waves) return;
-  unsigned char* base = smem + (size_t)wib * kPool * kSlotBytes;
-  uint32_t* s_seed = reinterpret_cast<uint32_t*>(base);
-  float* s_r = reinterpret_cast<float*>(s_seed + kPool);
-  float* s_g = s_r + kPool;
-  float* s_b = s_g + kPool;
-  uint32_t* s_samples = reinterpret_cast<uint32_t*>(s_b + kPool);
-  uint32_t* s_live = s_samples + kPool;
-  uint16_t* s_rem = reinterpret_cast<uint16_t*>(s_live + kPool);
-  uint16_t* q_ready = s_rem + kPool;
-  uint16_t* q_ff = q_ready + kPool;
-
-  const uint32_t t1 = sc->which_t1, t2 = sc->which_t2;
-  const int D = p.depth, S = p.spp;
-  const int64_t left = p.npix - w;
-  const int n_slots = left <= 0 ? 0 : (int)min<int64_t>(kPool, (left + n_waves - 1) / n_waves);
-  for (int j = lane; j < n_slots; j += 64) {
-    const int64_t k = (int64_t)j * n_waves + w;
-    s_seed[j] = p.seed_base + (uint32_t)pixel_of<kTiles>(p, k);  // seeds[i] = i (MapperPathTracer.cxx:265-267)
-    s_r[j] = 0.f;
-    s_g[j] = 0.f;
-    s_b[j] = 0.f;
-    s_samples[j] = 0u;
-    s_live[j] = 0u;
-    s_rem[j] = 0;
-    q_ready[j] = (uint16_t)j;
-  }
-  wave_sync();
-  uint32_t ready_head = 0, ready_tail = (S > 0) ? n_slots : 0, ff_head = 0, ff_tail = 0;
-  float4* __restrict__ const hist_base = reinterpret_cast<float4*>(p.hist) + (int64_t)w * kPool;
-  const int64_t stride = (int64_t)n_waves * kPool;
-  uint32_t published = 0;
-  bool critical_ff = false;
-  const f3 eye = ld3(p.cam.eye);
-
-  bool has_a = false, has_b = false;
-  int slot_a = 0, slot_b = 0;
-  uint32_t seed_a = 0, seed_b = 0;
-  Path pa, pb;
-  pa.org = eye;
-  pa.dir = mk(0.f, 0.f, 1.f);
-  pa.d = 0;
-  pa.nonfinite = false;
-  pb = pa;
-
-  for (;;) {
-    const uint64_t idle_a = __ballot(!has_a), idle_b = __ballot(!has_b);
-    const int c_a = __popcll(idle_a);
-    const int n_idle = c_a + __popcll(idle_b);
-    const int n_ready = (int)(ready_tail - ready_head);
-    const int n_ff = (int)(ff_tail - ff_head);
-    if ((n_ready < n_idle + RTP_FF_MARGIN || critical_ff) && n_ff > 0) {
-      critical_ff = false;
-      // ---- batch RNG fast-forward (pool_body's, without its diagnostics) ----
-      const int n = min(64, n_ff);
-      const bool mine = lane < n;
-      int fslot = 0, frem = 0;
-      uint32_t fseed = 0;
-      if (mine) {
-        fslot = q_ff[(ff_head + lane) & (kPool - 1)];
-        fseed = s_seed[fslot];
-        frem = s_rem[fslot];
-      }
-      uint32_t early = 0;
-      const int frc = frem & kRemMask;
-      CKP& FP = kparams();
-      const bool has_direct = mine && FP.ffd != nullptr && (unsigned)(frc - FP.ffd_first) < (unsigned)FP.ffd_count;
-      const bool has_early = mine && !has_direct && FP.ff[0] != nullptr && frc >= 32;
-      if (has_direct || has_early) {
-        GU32* src = (GU32*)(has_direct ? FP.ffd + ((uint64_t)(frc - FP.ffd_first) << 32) : FP.ff[0]);
-        early = src[fseed];
-      }
-      if (mine) {
-        const int flags = frem;
-        frem &= kRemMask;
-        f3 c;
-        if (flags & kEndLight) {
-          const int k_end = D - frem;
-          const float4* __restrict__ hp = hist_base + fslot;
-          f3 rw[kHistPrefetch];
-#pragma unroll
-          for (int i = 0; i < kHistPrefetch; i++) {
-            const float4 v = hp[(int64_t)max(k_end - i, 0) * stride];
-            rw[i] = mk(v.x, v.y, v.z);
-          }
-          float sx = rw[0].x + 0.0f, sy = rw[0].y + 0.0f, sz = rw[0].z + 0.0f;
-#pragma unroll
-          for (int i = 1; i < kHistPrefetch; i++) {
-            const bool on = k_end - i >= 0;
-            sx = on ? 0.0f + rw[i].x * sx : sx;
-            sy = on ? 0.0f + rw[i].y * sy : sy;
-            sz = on ? 0.0f + rw[i].z * sz : sz;
-          }
-          for (int dd = k_end - kHistPrefetch; dd >= 0; dd -= kHistChunk) {
-            f3 rc[kHistChunk];
-#pragma unroll
-            for (int i = 0; i < kHistChunk; i++) {
-              const float4 v = hp[(int64_t)max(dd - i, 0) * stride];
-              rc[i] = mk(v.x, v.y, v.z);
-            }
-#pragma unroll
-            for (int i = 0; i < kHistChunk; i++) {
-              const bool on = dd - i >= 0;
-              sx = on ? 0.0f + rc[i].x * sx : sx;
-              sy = on ? 0.0f + rc[i].y * sy : sy;
-              sz = on ? 0.0f + rc[i].z * sz : sz;
-            }
-          }
-          c = mk(sx, sy, sz);
-        } else {
-          const float v = (flags & kEndNonfinite) ? __builtin_nanf("") : 0.0f;
-          c = mk(v, v, v);
-        }
-        s_r[fslot] = s_r[fslot] + c.x;  // cols += sumtotl (MapperPathTracer.cxx:350), in sample order
-        s_g[fslot] = s_g[fslot] + c.y;
-        s_b[fslot] = s_b[fslot] + c.z;
-      }
-      if (has_direct) {
-        fseed = early;
-        frem = 0;
-      } else if (has_early) {
-        fseed = early;
-        frem -= 32;
-      }
-#pragma unroll
-      for (int j = 1; j < kFfTables; j++) {
-        GU32* __restrict__ tab = (GU32*)kparams().ff[j];
-        if (tab != nullptr && mine && frem >= (32 >> j)) {
-          fseed = tab[fseed];
-          frem -= 32 >> j;
-        }
-      }
-      for (int i = 0;; i++) {
-        const bool act = mine && i < frem;
-        if (!__any(act)) break;
-        if (act) fseed = dead_step(fseed, t1, t2);
-      }
-      bool again = false;
-      if (mine) s_seed[fslot] = fseed;
-      if (mine) again = s_samples[fslot] < (uint32_t)S;
-      const bool urgent = again && s_samples[fslot] * (uint32_t)n_slots <= (uint32_t)ff_tail;
-      const uint64_t pu = __ballot(urgent), pn = __ballot(again && !urgent);
-      ready_head -= (uint32_t)__popcll(pu);
-      if (urgent) q_ready[(ready_head + lane_rank(pu)) & (kPool - 1)] = (uint16_t)fslot;
-      if (again && !urgent) q_ready[(ready_tail + lane_rank(pn)) & (kPool - 1)] = (uint16_t)fslot;
-      ready_tail += __popcll(pn);
-      ff_head += n;
-      wave_sync();
-    }
-    // ---- refill idle paths (A's first, then B's) with READY pixels ----
-    const int take = min(n_idle, (int)(ready_tail - ready_head));
-    {
-      CKP& P = kparams();
-      if (!has_a) {
-        const int r = (int)lane_rank(idle_a);
-        if (r < take) {
-          slot_a = q_ready[(ready_head + r) & (kPool - 1)];
-          seed_a = s_seed[slot_a];
-          int pi, pj;
-          pixel_xy<kTiles>(P, slot_a * n_waves + w, pi, pj);
-          pa.dir = camera_ray(P.cam, pi, pj, P.nx, P.ny, seed_a);
-          pa.org = ld3(P.cam.eye);
-          pa.d = 0;
-          pa.nonfinite = false;
-          has_a = true;
-        }
-      }
-      if (!has_b) {
-        const int r = c_a + (int)lane_rank(idle_b);
-        if (r < take) {
-          slot_b = q_ready[(ready_head + r) & (kPool - 1)];
-          seed_b = s_seed[slot_b];
-          int pi, pj;
-          pixel_xy<kTiles>(P, slot_b * n_waves + w, pi, pj);
-          pb.dir = camera_ray(P.cam, pi, pj, P.nx, P.ny, seed_b);
-          pb.org = ld3(P.cam.eye);
-          pb.d = 0;
-          pb.nonfinite = false;
-          has_b = true;
-        }
-      }
-    }
-    ready_head += take;
-    if (!__any(has_a | has_b) && ff_tail == ff_head) break;
-    // ---- one depth of both paths: one closest-hit pass, then each shade ----
-    Hit ha, hb;
-    closest_hit2(sc, pa.org, pa.dir, ha, has_a, pb.org, pb.dir, hb, has_b, s_qshade + kPrexLdsOffset);
-    bool end_a = false, end_b = false;
-    auto step = [&](Path& ps, uint32_t& seed, int slot, const Hit& h, bool& has, bool& ended) {
-      f3 emit = mk(0.f, 0.f, 0.f);
-      float4* const hist = hist_base + slot;
-      const int res = shade_hit<false, true>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D, s_qshade, h);
-      if (res == kAlive && ps.d < D - 1) {
-        ps.d++;
-      } else {
-        const int k_end = ps.d;
-        if (res == kLight) hist[(int64_t)k_end * stride] = make_float4(emit.x, emit.y, emit.z, 0.f);
-        const int rem = D - 1 - k_end + (res != kAlive ? 1 : 0);
-        s_rem[slot] = (uint16_t)(rem | (res == kLight ? kEndLight : 0) | (ps.nonfinite ? kEndNonfinite : 0));
-        s_samples[slot] = s_samples[slot] + 1u;
-        s_live[slot] = s_live[slot] + (uint32_t)(k_end + 1);
-        s_seed[slot] = seed;
-        ended = true;
-        has = false;
-      }
-    };
-    if (has_a) step(pa, seed_a, slot_a, ha, has_a, end_a);
-    if (has_b) step(pb, seed_b, slot_b, hb, has_b, end_b);
-    const uint64_t fin_a = __ballot(end_a), fin_b = __ballot(end_b);
-    const int nf_a = __popcll(fin_a);
-    if (end_a) q_ff[(ff_tail + lane_rank(fin_a)) & (kPool - 1)] = (uint16_t)slot_a;
-    if (end_b) q_ff[(ff_tail + nf_a + lane_rank(fin_b)) & (kPool - 1)] = (uint16_t)slot_b;
-#if RTP_CRIT_FF > 0
-    {
-      const float lim = (float)ff_tail * (float)(1000 - RTP_CRIT_FF);
-      const bool ca = end_a && (float)(s_samples[slot_a] * (uint32_t)n_slots) * 1000.0f < lim;
-      const bool cb = end_b && (float)(s_samples[slot_b] * (uint32_t)n_slots) * 1000.0f < lim;
-      if (__ballot(ca | cb)) critical_ff = true;
-    }
-#endif
-    ff_tail += nf_a + __popcll(fin_b);
-    wave_sync();
-    if (RTP_PRIO_BALANCE && ff_tail - published >= (uint32_t)kPrioPeriod) {
-      unsigned long long g = 0;
-      if (lane == 0) g = atomicAdd(kparams().progress, (unsigned long long)(ff_tail - published));
-      g = __shfl(g, 0) + (unsigned long long)(ff_tail - published);
-      published = ff_tail;
-      set_priority(((float)g / (float)kparams().npix - (float)ff_tail / (float)n_slots) / (float)S);
-    }
-  }
-  wave_sync();
-  for (int j = lane; j < n_slots; j += 64) {
-    const int64_t k = (int64_t)j * n_waves + w;
-    reinterpret_cast<float4*>(p.out)[k] = make_float4(s_r[j], s_g[j], s_b[j], 0.f);
-    if (p.seed_out) p.seed_out[k] = s_seed[j];
-    if (p.live_out) p.live_out[k] = s_live[j];
-  }
-}
-#ifndef RTP_PAIR_MIN_WAVES_PER_EU
-#define RTP_PAIR_MIN_WAVES_PER_EU 2
-#endif
-template <bool kTiles>
-__global__ void __launch_bounds__(256, RTP_PAIR_MIN_WAVES_PER_EU)
-    rtp_render_pool_pair(const DevScene* __restrict__ sc, KParams p, int n_waves) {
-  __shared__ __align__(16) unsigned char smem[kPoolLdsBytes];
-  __shared__ __align__(16) float s_qshade[kQTableFloats];
-  pool_body_pair<kTiles>(sc, p, n_waves, smem, s_qshade);
-}
-
 // Scenes whose LDS walk tree fits (DevScene::lw_nodes, rtp_lds_walk_capacity):
 // one 16-wave block per CU (4 waves per SIMD, <= 128 VGPRs) shares one LDS
 // copy of the tree -- dynamic LDS after the waves' pools, the quad tables and
@@ -2150,21 +1714,6 @@ extern "C" int rtp_plan_steal(int64_t npix, int bvh) {
   return std::min<int>((int)resident, steal_resident_waves(bvh));
 }
 
-// Waves of rtp_render_pool_pair that fit the chip at once (its own
-// occupancy, the smaller of the contiguous and tile-deal instances).
-extern "C" int rtp_pair_resident_waves(void) {
-  static int cached = -1;
-  if (cached > 0) return cached;
-  int dev = 0, cus = 0, a = 0, b = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, rtp::rtp_render_pool_pair<false>, 256, 0) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtp::rtp_render_pool_pair<true>, 256, 0) != hipSuccess)
-    return 0;
-  cached = cus * std::max(1, std::min(a, b)) * rtp::kWavesPerBlock;
-  return cached;
-}
-
 // Bytes of LDS the LDS walk's tree may take (nodes of 8 octant copies plus
 // the leaf spheres, 16 B each): what the 16-wave block leaves of the CU's 160 KiB.
 extern "C" int rtp_lds_walk_capacity(void) { return std::max(0, rtp::kLdsWalkDynBytes); }
@@ -2187,11 +1736,6 @@ extern "C" hipError_t rtp_launch_render(const rtp::DevScene* scene, const rtp::K
       hipLaunchKernelGGL(rtp::rtp_render_lockstep<true>, dim3((unsigned)grid), dim3(256), 0, stream, scene, *p);
     else
       hipLaunchKernelGGL(rtp::rtp_render_lockstep<false>, dim3((unsigned)grid), dim3(256), 0, stream, scene, *p);
-  } else if (variant == 3) {  // two paths per lane (rtp_render_pool_pair): no BVH, no plan, no stealing
-    if (bvh || p->wave_begin || (int64_t)waves * rtp::kPool < p->npix) return hipErrorNotSupported;
-    const dim3 g((unsigned)((waves + rtp::kWavesPerBlock - 1) / rtp::kWavesPerBlock)), b(256);
-    if (p->tile_world > 0) hipLaunchKernelGGL((rtp::rtp_render_pool_pair<true>), g, b, 0, stream, scene, *p, waves);
-    else hipLaunchKernelGGL((rtp::rtp_render_pool_pair<false>), g, b, 0, stream, scene, *p, waves);
   } else if (bvh == 2) {  // the sphere BVH walked out of LDS
     if (p->wave_begin || lds_bytes <= 0 || lds_bytes > rtp::kLdsWalkDynBytes) return hipErrorNotSupported;
     (void)lds_bvh_resident_blocks_per_cu();  // (sets the kernels' dynamic-LDS limit once)

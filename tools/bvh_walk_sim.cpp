@@ -13,7 +13,8 @@
 //             every child box tested per visit, hit children visited near to
 //             far through a stack, sphere leaves tested after their box.
 // Prints per-ray means: node visits, box tests, sphere tests, max stack depth,
-// and the layout sizes.  build: g++ -O2 -std=c++17 tools/bvh_walk_sim.cpp
+// and the layout sizes.  `bvh_walk_sim <rays> builders`: one-sphere leaves
+// built with 16 / 32 / 64 bins or a full sweep SAH, threaded visits per ray.  build: g++ -O2 -std=c++17 tools/bvh_walk_sim.cpp
 //   -Iinclude -Lraytracingtherestofyourlife_amd -lrtp -Wl,-rpath,$PWD/raytracingtherestofyourlife_amd
 #include <algorithm>
 #include <cmath>
@@ -107,6 +108,122 @@ static int build(std::vector<Prim>& P, int b, int e, std::vector<Node>& T, std::
   return me;
 }
 
+// the same recursion with B bins per axis, or B = 0: a full sweep (every
+// split between centroid-sorted neighbours on each axis, ties by index)
+static int build_b(std::vector<Prim>& P, int b, int e, std::vector<Node>& T, std::vector<int>& order, int B, int depth) {
+  if (B > 0 && B != 16) {
+    // binned with B bins (copy of build()'s logic with a runtime bin count)
+    const int me = (int)T.size();
+    T.emplace_back();
+    Node nd;
+    nd.depth = depth;
+    float clo[3], chi[3];
+    for (int k = 0; k < 3; k++) nd.lo[k] = clo[k] = INFINITY, nd.hi[k] = chi[k] = -INFINITY;
+    for (int i = b; i < e; i++)
+      for (int k = 0; k < 3; k++) {
+        nd.lo[k] = std::min(nd.lo[k], P[i].lo[k]), nd.hi[k] = std::max(nd.hi[k], P[i].hi[k]);
+        clo[k] = std::min(clo[k], P[i].cen[k]), chi[k] = std::max(chi[k], P[i].cen[k]);
+      }
+    const int n = e - b;
+    if (n <= 1) {
+      nd.first = (int)order.size();
+      nd.count = n;
+      for (int i = b; i < e; i++) order.push_back(P[i].idx);
+      T[me] = nd;
+      return me;
+    }
+    int best_ax = -1, best_split = 0;
+    float best_cost = INFINITY;
+    std::vector<int> cnt(B);
+    std::vector<float> blo(3 * B), bhi(3 * B);
+    for (int ax = 0; ax < 3; ax++) {
+      const float ext = chi[ax] - clo[ax];
+      if (!(ext > 0)) continue;
+      std::fill(cnt.begin(), cnt.end(), 0);
+      std::fill(blo.begin(), blo.end(), INFINITY);
+      std::fill(bhi.begin(), bhi.end(), -INFINITY);
+      for (int i = b; i < e; i++) {
+        const int j = std::min(B - 1, std::max(0, (int)((P[i].cen[ax] - clo[ax]) / ext * B)));
+        cnt[j]++;
+        for (int k = 0; k < 3; k++) blo[3 * j + k] = std::min(blo[3 * j + k], P[i].lo[k]), bhi[3 * j + k] = std::max(bhi[3 * j + k], P[i].hi[k]);
+      }
+      for (int sp = 1; sp < B; sp++) {
+        float llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        float rlo[3] = {INFINITY, INFINITY, INFINITY}, rhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        int nl = 0, nr = 0;
+        for (int j = 0; j < B; j++) {
+          if (!cnt[j]) continue;
+          float* lo = j < sp ? llo : rlo;
+          float* hi = j < sp ? lhi : rhi;
+          (j < sp ? nl : nr) += cnt[j];
+          for (int k = 0; k < 3; k++) lo[k] = std::min(lo[k], blo[3 * j + k]), hi[k] = std::max(hi[k], bhi[3 * j + k]);
+        }
+        if (!nl || !nr) continue;
+        const float cost = nl * half_area(llo, lhi) + nr * half_area(rlo, rhi);
+        if (cost < best_cost) best_cost = cost, best_ax = ax, best_split = sp;
+      }
+    }
+    int mid = b + n / 2;
+    if (best_ax >= 0) {
+      const int ax = best_ax;
+      const float ext = chi[ax] - clo[ax];
+      mid = (int)(std::stable_partition(P.begin() + b, P.begin() + e, [&](const Prim& x) {
+                    return std::min(B - 1, std::max(0, (int)((x.cen[ax] - clo[ax]) / ext * B))) < best_split;
+                  }) - P.begin());
+      nd.axis = ax;
+    }
+    nd.left = build_b(P, b, mid, T, order, B, depth + 1);
+    nd.right = build_b(P, mid, e, T, order, B, depth + 1);
+    T[me] = nd;
+    return me;
+  }
+  if (B == 16) return build(P, b, e, T, order, 1, depth);
+  // full sweep
+  const int me = (int)T.size();
+  T.emplace_back();
+  Node nd;
+  nd.depth = depth;
+  for (int k = 0; k < 3; k++) nd.lo[k] = INFINITY, nd.hi[k] = -INFINITY;
+  for (int i = b; i < e; i++)
+    for (int k = 0; k < 3; k++) nd.lo[k] = std::min(nd.lo[k], P[i].lo[k]), nd.hi[k] = std::max(nd.hi[k], P[i].hi[k]);
+  const int n = e - b;
+  if (n <= 1) {
+    nd.first = (int)order.size();
+    nd.count = n;
+    for (int i = b; i < e; i++) order.push_back(P[i].idx);
+    T[me] = nd;
+    return me;
+  }
+  int best_ax = 0, best_i = n / 2;
+  float best_cost = INFINITY;
+  std::vector<float> racc(n);
+  for (int ax = 0; ax < 3; ax++) {
+    std::sort(P.begin() + b, P.begin() + e, [ax](const Prim& x, const Prim& y) {
+      return x.cen[ax] < y.cen[ax] || (x.cen[ax] == y.cen[ax] && x.idx < y.idx);
+    });
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = n - 1; i >= 1; i--) {  // right boxes: prims [i, n)
+      for (int k = 0; k < 3; k++) lo[k] = std::min(lo[k], P[b + i].lo[k]), hi[k] = std::max(hi[k], P[b + i].hi[k]);
+      racc[i] = (n - i) * half_area(lo, hi);
+    }
+    for (int k = 0; k < 3; k++) lo[k] = INFINITY, hi[k] = -INFINITY;
+    for (int i = 1; i < n; i++) {  // left: prims [0, i)
+      for (int k = 0; k < 3; k++) lo[k] = std::min(lo[k], P[b + i - 1].lo[k]), hi[k] = std::max(hi[k], P[b + i - 1].hi[k]);
+      const float cost = i * half_area(lo, hi) + racc[i];
+      if (cost < best_cost) best_cost = cost, best_ax = ax, best_i = i;
+    }
+  }
+  const int ax = best_ax;
+  std::sort(P.begin() + b, P.begin() + e, [ax](const Prim& x, const Prim& y) {
+    return x.cen[ax] < y.cen[ax] || (x.cen[ax] == y.cen[ax] && x.idx < y.idx);
+  });
+  nd.axis = ax;
+  nd.left = build_b(P, b, b + best_i, T, order, B, depth + 1);
+  nd.right = build_b(P, b + best_i, e, T, order, B, depth + 1);
+  T[me] = nd;
+  return me;
+}
+
 struct Sph {
   float c[3], r, rr;
 };
@@ -192,6 +309,50 @@ int main(int argc, char** argv) {
     return t;
   };
   printf("# C3 scene: %d spheres; %d rays from points in the room\n", d.n_spheres, nrays);
+  if (argc > 2 && !strcmp(argv[2], "builders")) {  // one-sphere leaves: the tree builder's effect on the threaded walk
+    for (int B : {16, 32, 64, 0}) {
+      std::vector<Prim> P(S.size());
+      for (size_t k = 0; k < S.size(); k++) {
+        const float pad = 0.002f * S[k].r + 1e-5f;
+        for (int a = 0; a < 3; a++)
+          P[k].lo[a] = S[k].c[a] - S[k].r - pad, P[k].hi[a] = S[k].c[a] + S[k].r + pad, P[k].cen[a] = S[k].c[a];
+        P[k].idx = (int)k;
+      }
+      std::vector<Node> T;
+      std::vector<int> order;
+      build_b(P, 0, (int)P.size(), T, order, B, 0);
+      double sah = 0, v = 0, sp = 0;
+      for (const Node& nd : T) sah += nd.left < 0 ? 0.0 : half_area(nd.lo, nd.hi);
+      sah /= half_area(T[0].lo, T[0].hi);
+      for (int r2 = 0; r2 < nrays; r2++) {
+        const float* o2 = &rays[6 * r2];
+        const float* d2 = o2 + 3;
+        const float inv2[3] = {1.f / d2[0], 1.f / d2[1], 1.f / d2[2]};
+        float best = wall_t(o2, d2);
+        std::vector<int> stk{0};
+        while (!stk.empty()) {
+          const int i = stk.back();
+          stk.pop_back();
+          const Node& nd = T[i];
+          v++;
+          if (nd.left < 0) {
+            float t;
+            sp++;
+            if (sphere_t(o2, d2, S[order[nd.first]], t) && t < best) best = t;
+            continue;
+          }
+          float tn;
+          if (!box_hit(o2, inv2, nd.lo, nd.hi, best, tn)) continue;
+          const bool neg = d2[nd.axis] < 0;
+          stk.push_back(neg ? nd.left : nd.right);
+          stk.push_back(neg ? nd.right : nd.left);
+        }
+      }
+      printf("builder %s%d: inner-node area sum / root %.2f | threaded walk %.2f visits %.2f sphere tests per ray\n",
+             B ? "binned " : "sweep", B, sah, v / nrays, sp / nrays);
+    }
+    return 0;
+  }
   for (int leaf : {1, 2, 3, 4, 6}) {
     std::vector<Prim> P(S.size());
     for (size_t k = 0; k < S.size(); k++) {

@@ -175,6 +175,176 @@ RTP_DEV Hit closest_hit_split(const DevScene* __restrict__ sc, f3 o, f3 d, const
   return h;
 }
 
+// ---- two rays per lane in one instruction stream (modes 11-13) ----
+// closest_hit<false> for rays A and B together: every scalar-loaded quad head
+// and prefilter record is tested against both rays, so the two rays'
+// dependent chains can interleave (ILP in place of a second wave on a SIMD
+// that a short launch leaves half empty).  Same keys, same minimum as two
+// closest_hit calls (mode 13).  act_a / act_b: the lane carries that ray.
+// (r04v: a pool kernel with two paths per lane built on this,
+// rtp_render_pool_pair in git 9f948ac, was 44-47% slower on C4's 1/8 and
+// 1/4 shares)
+template <int K>
+RTP_DEV void scan_kind_pf2(const DevScene* __restrict__ sc, int b, int e, f3 oa, f3 da, uint64_t& ba, f3 ob, f3 db,
+                           uint64_t& bb, u16v& cur) {
+  const DevQuad* qp = sc->quads + b;
+  for (int n = e - b; n > 0; n -= 2, qp += 2) {
+    const u16v nxt = head_at(qp + 1);
+    scan_one<K>(qp[0], cur, oa, da, ba);
+    scan_one<K>(qp[0], cur, ob, db, bb);
+    if (n == 1) {
+      cur = nxt;
+      break;
+    }
+    cur = head_at(qp + 2);
+    scan_one<K>(qp[1], nxt, oa, da, ba);
+    scan_one<K>(qp[1], nxt, ob, db, bb);
+  }
+}
+struct PreRay {
+  float inv, oa, ma, mb;
+  f2v obc, dbc;
+  uint32_t k1, k2;
+};
+template <int A>
+RTP_DEV void pre_setup(PreRay& r, f3 o, f3 d) {
+  constexpr int B = (A + 1) % 3, C = (A + 2) % 3;
+  r.inv = __builtin_amdgcn_rcpf(comp<A>(d));
+  r.oa = comp<A>(o);
+  r.obc = f2v{comp<B>(o), comp<C>(o)};
+  r.dbc = f2v{comp<B>(d), comp<C>(d)};
+}
+RTP_DEV void pre_fold(PreRay& r, const PreQuad& P) {
+  const float t = (P.x - r.oa) * r.inv;
+  const f2v u = __builtin_elementwise_fma(f2v{t, t}, r.dbc, r.obc) - f2v{P.cb, P.cc};
+  const float ub = fabsf(u.x) - P.rb, uc = fabsf(u.y) - P.rc;
+  const float m = __builtin_fmaf(fabsf(t), r.ma, r.mb);
+  const bool ok = (fmaxf(ub, uc) <= m) & (t > kPreTmin);
+  uint32_t key;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(key) : "v"(__float_as_uint(t - m)), "v"(~31u), "s"((uint32_t)P.qpos));
+  key = ok ? key : ~0u;
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r.k2) : "v"(r.k1), "v"(r.k2), "v"(key));
+  r.k1 = min(r.k1, key);
+}
+template <int A>
+RTP_DEV void pre_axis2(const DevScene* __restrict__ sc, int b, int e, f3 oa, f3 da, PreRay& ra, f3 ob, f3 db, PreRay& rb,
+                       u8v& cur) {
+  if (b == e) return;
+  pre_setup<A>(ra, oa, da);
+  pre_setup<A>(rb, ob, db);
+  auto as_pre = [](const u8v& v) {
+    PreQuad P;
+    __builtin_memcpy(&P, &v, sizeof(P));
+    return P;
+  };
+  const PreQuad* pq = sc->pre + b;
+  for (int n = e - b; n > 0; n -= 2, pq += 2) {
+    const u8v nxt = *reinterpret_cast<const u8v*>(pq + 1);
+    const PreQuad P0 = as_pre(cur);
+    pre_fold(ra, P0);
+    pre_fold(rb, P0);
+    if (n == 1) {
+      cur = nxt;
+      break;
+    }
+    cur = *reinterpret_cast<const u8v*>(pq + 2);
+    const PreQuad P1 = as_pre(nxt);
+    pre_fold(ra, P1);
+    pre_fold(rb, P1);
+  }
+}
+RTP_DEV void pre_candidate(f3 o, f3 d, const PreRay& r, bool lane_ok, const float* lds_prex, uint64_t& key) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v* lx = reinterpret_cast<const f4v*>(lds_prex) + 4 * (r.k1 & 31u);
+  f4v xr[4] = {lx[0], lx[1], lx[2], lx[3]};
+  if (lane_ok && r.k1 != ~0u) {
+    PreExact Q;
+    __builtin_memcpy(&Q, xr, sizeof(Q));
+    float t;
+    const bool ok = quad_hit_axis(Q, o, d, t);
+    const uint64_t kq = (uint64_t)__float_as_uint(t) << 32 | Q.key_lo;
+    key = (ok && t > 0.001f && kq < key) ? kq : key;
+  }
+}
+RTP_DEV bool pre_lane_ok(f3 o, f3 d) {
+  return (int)(fabsf(o.x) <= kPreLimD) & (int)(fabsf(o.y) <= kPreLimD) & (int)(fabsf(o.z) <= kPreLimD) &
+         (int)(fabsf(d.x) <= kPreLimD) & (int)(fabsf(d.y) <= kPreLimD) & (int)(fabsf(d.z) <= kPreLimD);
+}
+RTP_DEV void pre_margins(const DevScene* __restrict__ sc, f3 o, f3 d, PreRay& r) {
+  const float dmax = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fmaxf(fabsf(d.z), 1.0f));
+  const float omax = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+  r.ma = kPreK * dmax;
+  r.mb = kPreK * (omax + (sc->pre_scale + 1.0f));
+  r.k1 = ~0u;
+  r.k2 = ~0u;
+}
+RTP_DEV Hit key_hit(const DevScene* __restrict__ sc, uint64_t key, f3 o, f3 d) {
+  Hit h{3.40282347e+38f, -1, 0};
+  if (key != kNoHitKey) {
+    h.t = __uint_as_float((uint32_t)(key >> 32));
+    h.kind = 0;
+    h.idx = (int)(key & 0xffu);
+  }
+  const int ns = sc->n_spheres;
+  for (int k = 0; k < ns; k++) {
+    const DevSphere& S = sc->spheres[k];
+    float t;
+    if (sphere_hit(o, d, 0.001f, h.t, ld3(S.c), S.rr, t)) {
+      h.t = t;
+      h.kind = 1;
+      h.idx = k;
+    }
+  }
+  return h;
+}
+RTP_DEV void closest_hit2(const DevScene* __restrict__ sc, f3 oa, f3 da, Hit& ha, bool act_a, f3 ob, f3 db, Hit& hb,
+                          bool act_b, const float* lds_prex) {
+  uint64_t ka = kNoHitKey, kb = kNoHitKey;
+  {
+    const int g6 = sc->kind_begin[6], g7 = sc->kind_begin[7], g8 = sc->kind_begin[8], g9 = sc->kind_begin[9],
+              g10 = sc->kind_begin[10], g11 = sc->kind_begin[11];
+    u16v cur = quad_head(sc, g6);
+    scan_kind_pf2<7>(sc, g6, g7, oa, da, ka, ob, db, kb, cur);
+    scan_kind_pf2<8>(sc, g7, g8, oa, da, ka, ob, db, kb, cur);
+    scan_kind_pf2<9>(sc, g8, g9, oa, da, ka, ob, db, kb, cur);
+    scan_kind_pf2<10>(sc, g9, g10, oa, da, ka, ob, db, kb, cur);
+    scan_kind_pf2<0>(sc, g10, g11, oa, da, ka, ob, db, kb, cur);
+  }
+  bool fa = true, fb = true;  // the lane needs the exact scan of the axis-plane quads for ray A / B
+  if (sc->n_pre > 0) {          // (wave-uniform)
+    const bool oka = pre_lane_ok(oa, da), okb = pre_lane_ok(ob, db);
+    PreRay ra, rb;
+    pre_margins(sc, oa, da, ra);
+    pre_margins(sc, ob, db, rb);
+    const int p0 = sc->pre_begin[0], p1 = sc->pre_begin[1], p2 = sc->pre_begin[2], p3 = sc->pre_begin[3];
+    u8v pcur = pre_rec(sc, p0);
+    pre_axis2<0>(sc, p0, p1, oa, da, ra, ob, db, rb, pcur);
+    pre_axis2<1>(sc, p1, p2, oa, da, ra, ob, db, rb, pcur);
+    pre_axis2<2>(sc, p2, p3, oa, da, ra, ob, db, rb, pcur);
+    pre_candidate(oa, da, ra, oka, lds_prex, ka);
+    pre_candidate(ob, db, rb, okb, lds_prex, kb);
+    fa = !oka || (ra.k2 & ~31u) <= (uint32_t)(ka >> 32);
+    fb = !okb || (rb.k2 & ~31u) <= (uint32_t)(kb >> 32);
+  }
+  fa = fa && act_a;
+  fb = fb && act_b;
+  if (__ballot(fa | fb)) {
+    if (fa | fb) {  // the exact scan for both rays (a full scan's minimum is the exact one either way)
+      const int g0 = sc->kind_begin[0], g1 = sc->kind_begin[1], g2 = sc->kind_begin[2], g3 = sc->kind_begin[3],
+                g4 = sc->kind_begin[4], g5 = sc->kind_begin[5], g6 = sc->kind_begin[6];
+      u16v cur = quad_head(sc, g0);
+      scan_kind_pf2<1>(sc, g0, g1, oa, da, ka, ob, db, kb, cur);
+      scan_kind_pf2<2>(sc, g1, g2, oa, da, ka, ob, db, kb, cur);
+      scan_kind_pf2<3>(sc, g2, g3, oa, da, ka, ob, db, kb, cur);
+      scan_kind_pf2<4>(sc, g3, g4, oa, da, ka, ob, db, kb, cur);
+      scan_kind_pf2<5>(sc, g4, g5, oa, da, ka, ob, db, kb, cur);
+      scan_kind_pf2<6>(sc, g5, g6, oa, da, ka, ob, db, kb, cur);
+    }
+  }
+  ha = key_hit(sc, ka, oa, da);
+  hb = key_hit(sc, kb, ob, db);
+}
+
 // the two parts of closest_hit (rtp_kernels.hip), each alone
 template <int kPart>
 RTP_DEV uint64_t ch_part(const DevScene* __restrict__ sc, f3 o, f3 d, const float* lds_prex) {
