@@ -268,22 +268,34 @@ def main() -> None:
     red = shard.OverlappedCanvasReduce(canvas, dist, overlap=(args.dist_backend == "nccl"),
                                        host_copy=(args.dist_backend != "nccl"), force=args.force_collective)
 
+    # the rank's tiles: computed in the kernel (rtp_render_tiles_device; C4's
+    # 1/8 share 263 vs 276 ms through the pixel list, profiles/r04y_*), which
+    # renders clipped edge tiles whole (C4's 1080 rows: 0.7% more work, not
+    # counted as samples): the entries inside the canvas are scattered
+    # (shard.tile_entries).  RTP_BENCH_LIST=1: the explicit pixel list.
+    tiled = (not contig) and os.environ.get("RTP_BENCH_LIST") != "1"
+    if tiled:
+        ent_np, pix_np = shard.tile_entries(nx, ny, rank, world)
+        assert np.array_equal(pix_np, ids_np)
+        n_tiles = len(range(rank, -(-nx // TILE) * -(-ny // TILE), world))
+        tile_out = torch.empty((TILE * TILE * n_tiles, 4), dtype=torch.float32, device="cuda")
+        whole = ent_np.size == tile_out.shape[0]
+        ent = None if whole else torch.from_numpy(ent_np).cuda()
+
     def gather_canvas():
+        if tiled:
+            return red.step(ids, tile_out if whole else tile_out.index_select(0, ent))
         return red.step(ids, out)
 
     def drain():
         red.drain()
-
-    # the rank's tiles: computed in the kernel (rtp_render_tiles_device) when
-    # the canvas is whole tiles, else the explicit pixel list
-    tiled = (not contig) and nx % TILE == 0 and ny % TILE == 0 and os.environ.get("RTP_BENCH_LIST") != "1"
 
     def render():
         if contig:
             dev.render_device(cam, nx, ny, args.spp, args.depth, out.data_ptr(), pixel_count=npix,
                               stream=stream.cuda_stream)
         elif tiled:
-            dev.render_tiles_device(cam, nx, ny, args.spp, args.depth, out.data_ptr(), rank, world,
+            dev.render_tiles_device(cam, nx, ny, args.spp, args.depth, tile_out.data_ptr(), rank, world,
                                     stream=stream.cuda_stream)
         else:
             dev.render_device(cam, nx, ny, args.spp, args.depth, out.data_ptr(), pixel_count=npix,
@@ -294,8 +306,8 @@ def main() -> None:
             dev.render_device(cam, nx, ny, args.spp, args.depth, out.data_ptr(), pixel_count=npix,
                               pixel_ids_ptr=0 if contig else ids.data_ptr(), stream=stream.cuda_stream,
                               live_ptr=live.data_ptr())
-        else:
-            render()
+            return red.step(ids, out)
+        render()
         return gather_canvas()
 
     t_first = time.perf_counter()

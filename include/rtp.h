@@ -124,8 +124,13 @@ rtp_status rtp_render(rtp_context* ctx, const rtp_camera* cam, int32_t nx, int32
  * `rank` of `world` owns tiles t = rank, rank + world, ... of the canvas in
  * row-major tile order, each tile's pixels row-major (the order of
  * shard.tile_pixels; the multi-GPU sharding of SURVEY.md 8(e)).
- * d_rgba_out: device float4[256 * tiles owned].  nx and ny must be multiples
- * of 16.  Equal to rtp_render_device with that pixel list, without the list. */
+ * d_rgba_out: device float4[256 * tiles owned]: entry 256 q + e is pixel
+ * (16 tx + e % 16, 16 ty + e / 16) of the rank's q-th tile (tx, ty).  A canvas
+ * that is not whole tiles (C4's 1080 rows) has clipped tiles on its right and
+ * top edges: their entries outside the canvas are rendered like the others
+ * (camera rays past the frame, seeds of no real pixel) and are to be ignored
+ * (shard.tile_entries).  Every entry inside the canvas equals
+ * rtp_render_device on that pixel, without a pixel list. */
 rtp_status rtp_render_tiles_device(rtp_context* ctx, const rtp_camera* cam, int32_t nx, int32_t ny, int32_t spp,
                                    int32_t depth, uint32_t seed_base, int32_t rank, int32_t world, float* d_rgba_out,
                                    void* hip_stream, rtp_stats* stats);

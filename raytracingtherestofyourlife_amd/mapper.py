@@ -330,7 +330,9 @@ class Device:
     def render_tiles_device(self, camera: Camera, nx: int, ny: int, spp: int, depth: int, out_ptr: int,
                             rank: int, world: int, seed_base: int = 0, stream: int = 0, timed: bool = False):
         """Device-resident render of rank's tiles of the round-robin 16x16
-        tile deal (out_ptr: device float4[256 * tiles], shard.tile_pixels order)."""
+        tile deal (out_ptr: device float4[256 * tiles owned], each tile whole;
+        on a canvas that is not whole tiles, shard.tile_entries gives the
+        entries inside the canvas and their pixels)."""
         st = RtpStats()
         cam = camera.to_c()
         check(self._L.rtp_render_tiles_device(self.handle, ctypes.byref(cam), nx, ny, spp, depth, seed_base, rank,

@@ -47,6 +47,27 @@ def tile_pixels(nx: int, ny: int, rank: int, world: int, tile: int = TILE) -> np
     return (rows * nx + cols)[keep]
 
 
+def tile_entries(nx: int, ny: int, rank: int, world: int, tile: int = TILE) -> tuple[np.ndarray, np.ndarray]:
+    """rtp_render_tiles_device's output layout: it renders the rank's tiles
+    whole (256 entries each, clipped edge tiles included), so its output has
+    256 * (tiles owned) entries.  Returns (entries, pixels): the indices of the
+    entries that lie inside the canvas and their pixel ids -- `pixels` equals
+    tile_pixels(nx, ny, rank, world), and out[entries] is its render."""
+    if nx <= 0 or ny <= 0:
+        raise ValueError("empty canvas")
+    if not 0 <= rank < world:
+        raise ValueError("rank out of range")
+    tx, ty = -(-nx // tile), -(-ny // tile)
+    tiles = np.arange(tx * ty)
+    mine = tiles[tiles % world == rank]
+    oy, ox = np.divmod(mine, tx)
+    ly, lx = np.divmod(np.arange(tile * tile), tile)
+    rows = (oy[:, None] * tile + ly[None, :]).astype(np.int64)
+    cols = (ox[:, None] * tile + lx[None, :]).astype(np.int64)
+    keep = ((rows < ny) & (cols < nx)).reshape(-1)
+    return np.flatnonzero(keep).astype(np.int64), (rows * nx + cols).reshape(-1)[keep]
+
+
 @dataclass(frozen=True)
 class SampleBatch:
     rank: int

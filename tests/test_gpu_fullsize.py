@@ -91,3 +91,36 @@ def test_full_canvas_on_the_stealing_schedule(device, tables_on, name, shard):
     got = (rgba[pos], sd[pos], lv[pos])
     want = (np.c_[g["rgb"][pix], np.zeros(pix.size, np.float32)], g["final_seed"][pix], g["live"][pix])
     assert_render_equal(got, want, f"{name} shard={shard}")
+
+
+@pytest.mark.parametrize("rank,world", [(0, 2), (5, 8)])
+def test_c4_share_through_the_tile_instance(device, tables_on, rank, world):
+    """bench.py's N > 1 path on C4's 1080 rows: rtp_render_tiles_device renders
+    the rank's tiles whole (clipped edge tiles included; the 1/2 share steals,
+    the 1/8 share does not), and the entries inside the canvas
+    (shard.tile_entries) match the c4_subset16k golden pixels bit for bit."""
+    import torch
+
+    import raytracingtherestofyourlife_amd as rtp
+    from _util import same_bits_or_both_nan
+    from raytracingtherestofyourlife_amd import shard as sh
+
+    g = _load("c4_subset16k")
+    nx, ny, spp, depth = int(g["nx"]), int(g["ny"]), int(g["spp"]), int(g["depth"])
+    assert int(g["variant"]) == 0 and int(g["seed_base"]) == 0 and ny % 16 != 0
+    ent, ids = sh.tile_entries(nx, ny, rank, world)
+    n_tiles = len(range(rank, -(-nx // 16) * -(-ny // 16), world))
+    out = torch.full((256 * n_tiles, 4), 5.0, dtype=torch.float32, device="cuda")
+    device.set_cornell_box(0)
+    device.render_tiles_device(rtp.default_camera(), nx, ny, spp, depth, out.data_ptr(), rank, world,
+                               stream=torch.cuda.current_stream().cuda_stream, timed=True)
+    torch.cuda.synchronize()
+    rgba = out.cpu().numpy()
+    assert not (rgba[:, 3] != 0).any(), "every entry of the owned tiles is written"
+    order = np.argsort(ids)
+    hit = np.isin(g["pixels"], ids)
+    pix = np.flatnonzero(hit)
+    pos = ent[order[np.searchsorted(ids[order], g["pixels"][hit])]]
+    assert pix.size > g["pixels"].size // (2 * world)
+    ok = same_bits_or_both_nan(rgba[pos, :3], g["rgb"][pix]).all(axis=1)
+    assert ok.all(), f"{int((~ok).sum())} of {pix.size} golden pixels differ"

@@ -10,8 +10,11 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("nx,ny,world,variant", [(64, 48, 1, 0), (64, 48, 2, 0), (80, 32, 3, 0), (48, 64, 5, 0),
-                                                  (64, 48, 3, 3)])
+                                                  (64, 48, 3, 3), (40, 30, 2, 0), (100, 36, 3, 0), (72, 40, 4, 3)])
 def test_gpu_tile_deal_equals_pixel_list(device, nx, ny, world, variant):
+    """Whole-tile canvases and clipped ones (the C4 case: 1080 rows): the
+    entries inside the canvas (shard.tile_entries) equal the pixel-list
+    render of shard.tile_pixels bit for bit."""
     import torch
 
     import raytracingtherestofyourlife_amd as rtp
@@ -20,30 +23,35 @@ def test_gpu_tile_deal_equals_pixel_list(device, nx, ny, world, variant):
     device.set_cornell_box(variant)  # 3: the 1000-sphere C3 scene (the BVH kernel instance)
     cam = rtp.default_camera()
     s = torch.cuda.current_stream().cuda_stream
+    tiles = -(-nx // 16) * -(-ny // 16)
     for rank in range(world):
         ids_np = shard.tile_pixels(nx, ny, rank, world)
+        ent, pix = shard.tile_entries(nx, ny, rank, world)
+        assert np.array_equal(pix, ids_np)
+        mine = len(range(rank, tiles, world))
         ids = torch.from_numpy(ids_np).cuda()
         a = torch.full((ids_np.size, 4), 7.0, dtype=torch.float32, device="cuda")
-        b = torch.full((ids_np.size, 4), 9.0, dtype=torch.float32, device="cuda")
+        b = torch.full((256 * mine + 64, 4), 9.0, dtype=torch.float32, device="cuda")  # (+64: no write past the tiles)
         device.render_device(cam, nx, ny, 5, 10, a.data_ptr(), pixel_count=ids_np.size, pixel_ids_ptr=ids.data_ptr(),
                              stream=s)
         device.render_tiles_device(cam, nx, ny, 5, 10, b.data_ptr(), rank, world, stream=s)
         torch.cuda.synchronize()
         an, bn = a.cpu().numpy(), b.cpu().numpy()
-        assert np.array_equal(an.view(np.uint32), bn.view(np.uint32)), (nx, ny, world, rank)
+        assert np.array_equal(an.view(np.uint32), bn[ent].view(np.uint32)), (nx, ny, world, rank)
+        assert (bn[256 * mine:] == 9.0).all(), "entries past the rank's tiles were written"
     device.set_cornell_box(0)
 
 
-def test_gpu_tile_deal_rejects_partial_tiles(device):
+def test_gpu_tile_deal_rejects_bad_rank(device):
     import torch
 
     import raytracingtherestofyourlife_amd as rtp
 
     out = torch.empty((256, 4), dtype=torch.float32, device="cuda")
     with pytest.raises(Exception):
-        device.render_tiles_device(rtp.default_camera(), 40, 32, 1, 5, out.data_ptr(), 0, 1)
-    with pytest.raises(Exception):
         device.render_tiles_device(rtp.default_camera(), 32, 32, 1, 5, out.data_ptr(), 2, 2)
+    with pytest.raises(Exception):
+        device.render_tiles_device(rtp.default_camera(), 32, 32, 1, 5, out.data_ptr(), -1, 2)
 
 
 def test_launch_rejects_more_than_int32_entries(device):

@@ -86,6 +86,28 @@ def test_tile_plan_covers_every_pixel_once():
         shard.tile_pixels(64, 64, 2, 2)
 
 
+def test_tile_entries_match_the_kernel_layout():
+    """rtp_render_tiles_device renders every owned tile whole: entry 256 q + e
+    is pixel (16 tx + e % 16, 16 ty + e // 16) of the q-th owned tile.
+    tile_entries picks the entries inside the canvas, in tile_pixels order."""
+    from raytracingtherestofyourlife_amd import shard
+
+    for nx, ny, world in ((1920, 1080, 8), (100, 64, 2), (17, 33, 3), (64, 48, 1)):
+        tx, ty = -(-nx // 16), -(-ny // 16)
+        for r in range(world):
+            ent, pix = shard.tile_entries(nx, ny, r, world)
+            assert np.array_equal(pix, shard.tile_pixels(nx, ny, r, world))
+            owned = np.arange(tx * ty)[r::world]
+            q, e = np.divmod(ent, 256)
+            ox, oy = owned[q] % tx, owned[q] // tx
+            assert np.array_equal(pix, (oy * 16 + e // 16) * nx + ox * 16 + e % 16)
+            assert ent.size == 0 or ent.max() < 256 * owned.size
+            if nx % 16 == 0 and ny % 16 == 0:
+                assert np.array_equal(ent, np.arange(256 * owned.size))
+    with pytest.raises(ValueError):
+        shard.tile_entries(64, 64, 2, 2)
+
+
 def test_sample_batches_partition():
     from raytracingtherestofyourlife_amd import shard
 

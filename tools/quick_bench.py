@@ -37,7 +37,9 @@ dev.set_cornell_box(a.variant)
 dev.set_ff_tables(a.ff_tables)
 cam = rtp.default_camera()
 n = a.nx * a.ny if ids is None else int(ids.numel())
-out = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
+# --tiles renders the rank's tiles whole (clipped edge tiles included)
+n_out = 256 * len(range(a.rank, -(-a.nx // 16) * -(-a.ny // 16), a.world)) if a.tiles else n
+out = torch.zeros((max(n, n_out), 4), dtype=torch.float32, device="cuda")
 live = torch.zeros(n, dtype=torch.int32, device="cuda")
 s = torch.cuda.current_stream().cuda_stream
 for r in range(a.reps):
@@ -55,7 +57,10 @@ for r in range(a.reps):
     wall = time.time() - t
     L = live.to(torch.int64).sum().item() / (n * a.spp)
     Lp = (live.to(torch.float64) / a.spp).cpu().numpy()
-    nr = n // a.world if a.tiles else n  # (--share: n is already the rank's pixels)
+    nr = n  # (--share: n is already the rank's pixels)
+    if a.tiles:  # the rank's pixels inside the canvas
+        from raytracingtherestofyourlife_amd import shard as _sh
+        nr = int(_sh.tile_pixels(a.nx, a.ny, a.rank, a.world).size)
     print(json.dumps(dict(rep=r, npix=nr, kernel_ms=st.kernel_ms, wall_s=wall, msamples_per_s=nr * a.spp / (st.kernel_ms / 1e3) / 1e6,
                           live_per_sample=L, nan_px=int(torch.isnan(out[:, :3]).any(1).sum().item()),
                           L_pixel_pct={q: round(float(np.percentile(Lp, q)), 3) for q in (50, 90, 99, 99.9, 100)})), flush=True)
