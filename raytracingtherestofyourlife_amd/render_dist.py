@@ -6,8 +6,9 @@ RCCL over xGMI, the shard plans of shard.py.
     ... --nx 3840 --ny 2160 --spp 16384 --shard samples --out c5.pnm
 
 --shard tiles (BASELINE configs[3], C4): 16x16 tiles round-robin over the
-    ranks; each rank renders its pixel list (rtp_render_device with the pixel
-    ids) into a zeroed canvas; one reduce(sum) to rank 0.  The image is
+    ranks; each rank renders its tiles (rtp_render_tiles_device: each entry's
+    pixel computed in the kernel) into a zeroed canvas; one reduce(sum) to
+    rank 0.  The image is
     bit-identical to a one-GPU render (x + 0 == x, NaN passes through).
 --shard samples (configs[4], C5): rank k renders spp_k samples of every
     pixel from the derived stream seed = pixel + k*N (shard.sample_batches);
@@ -74,8 +75,14 @@ def main(argv=None) -> int:
     canvas = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
 
     if a.shard == "tiles":
-        ids = torch.from_numpy(shard.tile_pixels(a.nx, a.ny, rank, world)).cuda()
-        part = torch.empty((ids.numel(), 4), dtype=torch.float32, device="cuda")
+        # the rank's tiles through the tile instance (each entry's pixel
+        # computed in the kernel, clipped edge tiles rendered whole); the
+        # entries inside the canvas go to their pixels (shard.tile_entries)
+        ent_np, ids_np = shard.tile_entries(a.nx, a.ny, rank, world)
+        ids = torch.from_numpy(ids_np).cuda()
+        ent = torch.from_numpy(ent_np).cuda()
+        n_tiles = len(range(rank, -(-a.nx // shard.TILE) * -(-a.ny // shard.TILE), world))
+        part = torch.empty((shard.TILE * shard.TILE * max(n_tiles, 1), 4), dtype=torch.float32, device="cuda")
         spp_mine, seed_base = a.spp, 0
     else:
         b = shard.sample_batches(a.spp, world, n)[rank]
@@ -99,12 +106,13 @@ def main(argv=None) -> int:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    st = dev.render_device(cam, a.nx, a.ny, spp_mine, a.depth, part.data_ptr(),
-                           pixel_count=(ids.numel() if ids is not None else n),
-                           pixel_ids_ptr=(ids.data_ptr() if ids is not None else 0), seed_base=seed_base,
-                           stream=stream.cuda_stream, timed=True)
     if ids is not None:
-        canvas.index_copy_(0, ids, part)
+        st = dev.render_tiles_device(cam, a.nx, a.ny, spp_mine, a.depth, part.data_ptr(), rank, world,
+                                     stream=stream.cuda_stream, timed=True)
+        canvas.index_copy_(0, ids, part.index_select(0, ent))
+    else:
+        st = dev.render_device(cam, a.nx, a.ny, spp_mine, a.depth, part.data_ptr(), pixel_count=n, seed_base=seed_base,
+                               stream=stream.cuda_stream, timed=True)
     reduce()
     torch.cuda.synchronize()
     if world > 1:
