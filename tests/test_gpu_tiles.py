@@ -42,6 +42,33 @@ def test_gpu_tile_deal_equals_pixel_list(device, nx, ny, world, variant):
     device.set_cornell_box(0)
 
 
+def test_gpu_tile_deal_rank_without_tiles(device):
+    """More ranks than tiles (a 40x20 canvas has 6 tiles, 8 ranks): ranks 6
+    and 7 own nothing -- the call succeeds and writes nothing; the others
+    still match the pixel list."""
+    import torch
+
+    import raytracingtherestofyourlife_amd as rtp
+    from raytracingtherestofyourlife_amd import shard
+
+    device.set_cornell_box(0)
+    cam = rtp.default_camera()
+    for rank in range(8):
+        ent, pix = shard.tile_entries(40, 20, rank, 8)
+        out = torch.full((256, 4), 3.0, dtype=torch.float32, device="cuda")
+        device.render_tiles_device(cam, 40, 20, 2, 5, out.data_ptr(), rank, 8)
+        torch.cuda.synchronize()
+        o = out.cpu().numpy()
+        if rank >= 6:
+            assert ent.size == 0 and (o == 3.0).all()
+            continue
+        ids = torch.from_numpy(pix).cuda()
+        a = torch.zeros((pix.size, 4), dtype=torch.float32, device="cuda")
+        device.render_device(cam, 40, 20, 2, 5, a.data_ptr(), pixel_count=pix.size, pixel_ids_ptr=ids.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(a.cpu().numpy().view(np.uint32), o[ent].view(np.uint32)), rank
+
+
 def test_gpu_tile_deal_rejects_bad_rank(device):
     import torch
 

@@ -104,6 +104,8 @@ def test_tile_entries_match_the_kernel_layout():
             assert ent.size == 0 or ent.max() < 256 * owned.size
             if nx % 16 == 0 and ny % 16 == 0:
                 assert np.array_equal(ent, np.arange(256 * owned.size))
+    ent, pix = shard.tile_entries(40, 20, 7, 8)  # 6 tiles, 8 ranks: rank 7 owns none
+    assert ent.size == 0 and pix.size == 0
     with pytest.raises(ValueError):
         shard.tile_entries(64, 64, 2, 2)
 
