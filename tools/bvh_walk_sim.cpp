@@ -309,6 +309,84 @@ int main(int argc, char** argv) {
     return t;
   };
   printf("# C3 scene: %d spheres; %d rays from points in the room\n", d.n_spheres, nrays);
+  if (argc > 2 && !strcmp(argv[2], "quant")) {
+    // binary "pair" nodes: a visit loads one 16-byte node holding BOTH
+    // children's boxes quantised to `bits` per coordinate on a grid over the
+    // root box (rounded outward), tests both, goes to the near hit child and
+    // pushes the far one; a sphere child is tested exactly at once (one more
+    // 16-byte load for its centre and r^2).  Loads per ray = node visits +
+    // sphere tests, against the threaded walk's one load per visit.
+    std::vector<Prim> P(S.size());
+    for (size_t k = 0; k < S.size(); k++) {
+      const float pad = 0.002f * S[k].r + 1e-5f;
+      for (int a = 0; a < 3; a++)
+        P[k].lo[a] = S[k].c[a] - S[k].r - pad, P[k].hi[a] = S[k].c[a] + S[k].r + pad, P[k].cen[a] = S[k].c[a];
+      P[k].idx = (int)k;
+    }
+    std::vector<Node> T;
+    std::vector<int> order;
+    build(P, 0, (int)P.size(), T, order, 1, 0);
+    for (int bits : {6, 8, 10, 16, 0}) {
+      std::vector<Node> Q = T;  // quantised boxes (bits 0: exact)
+      if (bits) {
+        const float cells = (float)((1 << bits) - 1);
+        for (Node& nd : Q)
+          for (int a = 0; a < 3; a++) {
+            const float lo0 = T[0].lo[a], ext = T[0].hi[a] - T[0].lo[a];
+            nd.lo[a] = lo0 + ext * std::floor((nd.lo[a] - lo0) / ext * cells) / cells;
+            nd.hi[a] = lo0 + ext * std::ceil((nd.hi[a] - lo0) / ext * cells) / cells;
+          }
+      }
+      double visits = 0, sph = 0;
+      int worst = 0;
+      for (int r2 = 0; r2 < nrays; r2++) {
+        const float* o2 = &rays[6 * r2];
+        const float* d2 = o2 + 3;
+        const float inv2[3] = {1.f / d2[0], 1.f / d2[1], 1.f / d2[2]};
+        float best = wall_t(o2, d2);
+        std::vector<std::pair<int, float>> stk;
+        int cur = 0, v = 0, sp = 0;
+        for (;;) {
+          if (cur >= 0) {
+            const Node& nd = Q[cur];
+            v++;
+            int nxt[2];
+            float tnx[2];
+            int nh = 0;
+            for (int c : {nd.left, nd.right}) {
+              float tn;
+              if (!box_hit(o2, inv2, Q[c].lo, Q[c].hi, best, tn)) continue;
+              if (Q[c].left < 0) {
+                float t;
+                sp++;
+                if (sphere_t(o2, d2, S[order[Q[c].first]], t) && t < best) best = t;
+                continue;
+              }
+              nxt[nh] = c, tnx[nh] = tn, nh++;
+            }
+            if (nh == 2) {
+              if (tnx[1] < tnx[0]) std::swap(nxt[0], nxt[1]), std::swap(tnx[0], tnx[1]);
+              stk.push_back({nxt[1], tnx[1]});
+              worst = std::max(worst, (int)stk.size());
+              cur = nxt[0];
+            } else {
+              cur = nh ? nxt[0] : -1;
+            }
+          } else {
+            if (stk.empty()) break;
+            auto e = stk.back();
+            stk.pop_back();
+            if (e.second <= best) cur = e.first;
+          }
+        }
+        visits += v;
+        sph += sp;
+      }
+      printf("pair nodes, boxes %s%d bits: %.2f node visits + %.2f sphere tests = %.2f 16-byte loads per ray (threaded: one per visit), max stack %d\n",
+             bits ? "" : "exact (", bits, visits / nrays, sph / nrays, (visits + sph) / nrays, worst);
+    }
+    return 0;
+  }
   if (argc > 2 && !strcmp(argv[2], "builders")) {  // one-sphere leaves: the tree builder's effect on the threaded walk
     for (int B : {16, 32, 64, 0}) {
       std::vector<Prim> P(S.size());
