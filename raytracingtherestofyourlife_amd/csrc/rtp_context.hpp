@@ -31,9 +31,6 @@ struct rtp_context {
   int32_t* d_lw_cidx = nullptr;
   float* d_lw_sph = nullptr;
   int32_t* d_lw_orig = nullptr;
-  uint32_t* d_pair_nodes = nullptr;  // pair-node experiment (DevScene::pair_nodes)
-  float* d_pair_sph = nullptr;
-  int32_t* d_pair_sidx = nullptr;
   int lw_bytes = 0;  // its LDS footprint (0: the scene has no LDS walk)
   bool use_bvh = false;
   int ff_policy = 0;  // rtp_ff_policy (RNG jump tables)

@@ -478,91 +478,6 @@ int bvh_build(std::vector<BvhPrim>& P, int b, int e, std::vector<TNode>& T, std:
   return me;
 }
 
-// Pair nodes (experiment, rtp_kernels.hip RTP_BVH_PAIR; DevScene::pair_nodes):
-// one 16-byte record per inner node (preorder ids, root 0) holding both
-// children's boxes as 8-bit coordinates on the grid x = org + q * scl over the
-// root box, rounded outward with the device's own decode (fmaf), and two
-// 16-bit child references (bit 15: a sphere, its position in the pair order).
-// A walk then loads one record per visit and tests two boxes: 19.9 loads per
-// C3 ray against the threaded walk's 36 (tools/bvh_walk_sim.cpp quant).
-struct PairTree {
-  std::vector<uint32_t> words;  // 4 per inner node
-  std::vector<float> sph;       // 4 per sphere (centre, r^2)
-  std::vector<int32_t> sidx;
-  float org[3], scl[3];
-};
-bool pair_build(const std::vector<TNode>& T, const std::vector<int32_t>& order, const std::vector<rtp::DevSphere>& sph,
-                PairTree& out) {
-  if (T.empty() || T[0].left < 0) return false;
-  std::vector<int> id(T.size(), -1);
-  int n_inner = 0;
-  std::vector<int> stk{0};
-  while (!stk.empty()) {  // preorder ids of the inner nodes
-    const int i = stk.back();
-    stk.pop_back();
-    if (T[i].left < 0) continue;
-    id[i] = n_inner++;
-    stk.push_back(T[i].right);
-    stk.push_back(T[i].left);
-  }
-  if (n_inner >= 0x7fff || (int64_t)order.size() >= 0x8000) return false;
-  {  // the walk's 12-entry stack holds at most depth - 1 deferred nodes
-    int depth = 0;
-    std::vector<std::pair<int, int>> st{{0, 1}};
-    while (!st.empty()) {
-      const auto [i, dd] = st.back();
-      st.pop_back();
-      depth = std::max(depth, dd);
-      if (T[i].left >= 0) st.push_back({T[i].left, dd + 1}), st.push_back({T[i].right, dd + 1});
-    }
-    if (depth - 1 > 12) return false;
-  }
-  for (int a = 0; a < 3; a++) {
-    out.org[a] = T[0].lo[a];
-    float scl = (T[0].hi[a] - T[0].lo[a]) / 255.0f;
-    if (!(scl > 0)) scl = 0x1p-20f;
-    while (std::fmaf(255.0f, scl, out.org[a]) < T[0].hi[a]) scl = std::nextafterf(scl, INFINITY);
-    out.scl[a] = scl;
-  }
-  auto dec = [&](int q, int a) { return std::fmaf((float)q, out.scl[a], out.org[a]); };
-  auto quant = [&](const TNode& b, uint8_t q[6]) {
-    for (int a = 0; a < 3; a++) {
-      int lo = std::max(0, std::min(255, (int)std::floor((b.lo[a] - out.org[a]) / out.scl[a])));
-      while (lo > 0 && dec(lo, a) > b.lo[a]) lo--;
-      int hi = std::max(0, std::min(255, (int)std::ceil((b.hi[a] - out.org[a]) / out.scl[a])));
-      while (hi < 255 && dec(hi, a) < b.hi[a]) hi++;
-      q[a] = (uint8_t)lo;
-      q[3 + a] = (uint8_t)hi;
-    }
-  };
-  out.words.assign((size_t)4 * n_inner, 0u);
-  out.sph.clear();
-  out.sidx.clear();
-  for (size_t i = 0; i < T.size(); i++) {
-    if (id[i] < 0) continue;
-    uint8_t bytes[16] = {};
-    uint32_t ref[2];
-    const int ch[2] = {T[i].left, T[i].right};
-    for (int c = 0; c < 2; c++) {
-      const TNode& C = T[ch[c]];
-      quant(C, bytes + 6 * c);
-      if (C.left < 0) {  // a sphere leaf (one sphere per leaf)
-        if (C.count != 1) return false;
-        const int k = order[C.first];
-        ref[c] = 0x8000u | (uint32_t)out.sidx.size();
-        out.sidx.push_back(k);
-        out.sph.insert(out.sph.end(), {sph[k].c[0], sph[k].c[1], sph[k].c[2], sph[k].rr});
-      } else {
-        ref[c] = (uint32_t)id[ch[c]];
-      }
-    }
-    uint32_t* w = &out.words[(size_t)4 * id[i]];
-    std::memcpy(w, bytes, 12);
-    w[3] = ref[0] | ref[1] << 16;
-  }
-  return true;
-}
-
 // inner nodes of the sphere BVH above this depth are dropped from the walks'
 // arrays (bvh_flatten below)
 constexpr int kBvhDropDepth = 2;
@@ -684,8 +599,7 @@ void rtp_destroy(rtp_context* c) {
   if (c->d_nodes) (void)hipFree(c->d_nodes);
   if (c->d_sph_geom) (void)hipFree(c->d_sph_geom);
   if (c->d_sph_all) (void)hipFree(c->d_sph_all);
-  for (void* p : {(void*)c->d_lw_nodes, (void*)c->d_lw_cidx, (void*)c->d_lw_sph, (void*)c->d_lw_orig,
-                  (void*)c->d_pair_nodes, (void*)c->d_pair_sph, (void*)c->d_pair_sidx})
+  for (void* p : {(void*)c->d_lw_nodes, (void*)c->d_lw_cidx, (void*)c->d_lw_sph, (void*)c->d_lw_orig})
     if (p) (void)hipFree(p);
   if (c->d_cnodes) (void)hipFree(c->d_cnodes);
   if (c->d_cidx) (void)hipFree(c->d_cidx);
@@ -826,7 +740,6 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
   std::vector<rtp::BvhNode> lw_nodes;
   std::vector<int32_t> lw_order;
   int lw_per_oct = 0;
-  PairTree pair;  // (experiment: RTP_BVH_PAIR)
   if (!use_bvh) {
     for (int k = 0; k < s->n_spheres; k++) h->spheres[k] = sph[k];
   } else if (gpu_build) {
@@ -850,7 +763,6 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     std::vector<int32_t> order;
     std::vector<TNode> tree;
     bvh_build(P, 0, s->n_spheres, tree, order);
-    if (!pair_build(tree, order, sph, pair)) pair.words.clear();
     // inner nodes above this depth are not emitted (bvh_flatten; RTP_BVH_DROP overrides)
     int drop = kBvhDropDepth;
     float drop_sa = kBvhDropArea;
@@ -949,7 +861,7 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
   }
   for (void** p : {(void**)&c->d_nodes, (void**)&c->d_sph_geom, (void**)&c->d_sph_all, (void**)&c->d_cnodes,
                    (void**)&c->d_cidx, (void**)&c->d_lw_nodes, (void**)&c->d_lw_cidx, (void**)&c->d_lw_sph,
-                   (void**)&c->d_lw_orig, (void**)&c->d_pair_nodes, (void**)&c->d_pair_sph, (void**)&c->d_pair_sidx})
+                   (void**)&c->d_lw_orig})
     if (*p && e == hipSuccess) {
       e = hipFree(*p);
       *p = nullptr;
@@ -991,19 +903,6 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     h->nodes = c->d_nodes;
     h->sph_geom = c->d_sph_geom;
     h->sph_all = c->d_sph_all;
-    if (e == hipSuccess && !pair.words.empty()) {  // the pair nodes (experiment)
-      e = hipMalloc(&c->d_pair_nodes, pair.words.size() * 4);
-      if (e == hipSuccess) e = hipMalloc(&c->d_pair_sph, pair.sph.size() * 4);
-      if (e == hipSuccess) e = hipMalloc(&c->d_pair_sidx, pair.sidx.size() * 4);
-      if (e == hipSuccess) e = hipMemcpy(c->d_pair_nodes, pair.words.data(), pair.words.size() * 4, hipMemcpyHostToDevice);
-      if (e == hipSuccess) e = hipMemcpy(c->d_pair_sph, pair.sph.data(), pair.sph.size() * 4, hipMemcpyHostToDevice);
-      if (e == hipSuccess) e = hipMemcpy(c->d_pair_sidx, pair.sidx.data(), pair.sidx.size() * 4, hipMemcpyHostToDevice);
-      h->pair_nodes = c->d_pair_nodes;
-      h->pair_sph = c->d_pair_sph;
-      h->pair_sidx = c->d_pair_sidx;
-      h->n_pair = (int32_t)(pair.words.size() / 4);
-      for (int a = 0; a < 3; a++) h->pair_org[a] = pair.org[a], h->pair_scl[a] = pair.scl[a];
-    }
     if (e == hipSuccess && lw_per_oct > 0) {  // the LDS walk's tree: compacted like the global one
       const int64_t total = (int64_t)8 * lw_per_oct, ns = (int64_t)lw_order.size();
       std::vector<float> lsph(4 * ns);

@@ -258,66 +258,6 @@ RTP_DEV int bvh_visit(GF4* __restrict__ geom_g, LF4* __restrict__ lsph, const Bv
   }
   return (hit || leaf) ? ni + 1 : (int)v.w;
 }
-#ifndef RTP_BVH_PAIR
-#define RTP_BVH_PAIR 0  // (experiment: the pair-node walk, DevScene::pair_nodes)
-#endif
-// One visit of the pair-node walk (experiment, RTP_BVH_PAIR): the record v
-// of the current node holds both children's 8-bit boxes on the grid
-// x = org + q * scl (rounded outward on the host with this decode) and their
-// references.  Each box is tested like bvh_visit's (same slab arithmetic and
-// slack, culling against the best hit so far); a hit sphere child is tested
-// exactly at once (hit kind 3: its pair-order position, scene index in
-// R.orig); the nearer hit inner child is entered and the farther pushed.
-// The stack is 12 16-bit entries in three 64-bit registers; the host builds
-// pair nodes only for trees of depth <= 13 (rtp_host.cpp pair_build), so it never
-// overflows (a depth-first walk holds at most depth - 1 deferred nodes).
-// Returns the next node, nn when the walk is done.
-RTP_DEV int pair_visit(GF4* __restrict__ psph, const BvhRay& R, const float (&org)[3], const float (&scl)[3], f3 o,
-                       f3 d, u4v v, Hit& h, uint64_t& s0, uint64_t& s1, uint64_t& s2, int nn) {
-  auto q = [&](int k) { return (float)((v[k >> 2] >> (8 * (k & 3))) & 0xffu); };
-  int in0 = nn, in1 = nn;
-  float tn0 = 0.f, tn1 = 0.f;
-#pragma unroll
-  for (int c = 0; c < 2; c++) {
-    const int b = 6 * c;
-    const float lx = __builtin_fmaf(q(b + 0), scl[0], org[0]), ly = __builtin_fmaf(q(b + 1), scl[1], org[1]);
-    const float lz = __builtin_fmaf(q(b + 2), scl[2], org[2]), hx = __builtin_fmaf(q(b + 3), scl[0], org[0]);
-    const float hy = __builtin_fmaf(q(b + 4), scl[1], org[1]), hz = __builtin_fmaf(q(b + 5), scl[2], org[2]);
-    const float x0 = __builtin_fmaf(lx, R.ix, R.ox), x1 = __builtin_fmaf(hx, R.ix, R.ox);
-    const float y0 = __builtin_fmaf(ly, R.iy, R.oy), y1 = __builtin_fmaf(hy, R.iy, R.oy);
-    const float z0 = __builtin_fmaf(lz, R.iz, R.oz), z1 = __builtin_fmaf(hz, R.iz, R.oz);
-    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
-    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
-    const float slack = 1e-5f * fabsf(tf) + 1e-7f;
-    const bool hit = tn <= tf + slack && tf >= 0.0f && tn <= h.t * 1.00001f + 1e-7f;
-    const uint32_t ref = (v.w >> (16 * c)) & 0xffffu;
-    if (hit && (ref & 0x8000u)) {  // a sphere child: its exact test now
-      const int j = (int)(ref & 0x7fffu);
-      const f4v g = psph[j];  // centre, r^2
-      float t;
-      if (sphere_root(o, d, 0.001f, mk(g.x, g.y, g.z), g.w, t)) bvh_accept(h, t, 3, j, R, [&] { return R.orig[j]; });
-    } else if (hit) {
-      if (c == 0) in0 = (int)ref, tn0 = tn;
-      else in1 = (int)ref, tn1 = tn;
-    }
-  }
-  if (in0 < nn && in1 < nn) {  // both: enter the nearer, push the farther
-    const bool first = tn0 <= tn1;
-    const int near = first ? in0 : in1, far = first ? in1 : in0;
-    s2 = (s2 << 16) | (s1 >> 48);
-    s1 = (s1 << 16) | (s0 >> 48);
-    s0 = (s0 << 16) | (uint64_t)(far + 1);  // (entries hold id + 1: 0 is empty)
-    return near;
-  }
-  if (in0 < nn) return in0;
-  if (in1 < nn) return in1;
-  const int top = (int)(s0 & 0xffffu);  // pop (0: the stack is empty, the walk is done)
-  s0 = (s0 >> 16) | (s1 << 48);
-  s1 = (s1 >> 16) | (s2 << 48);
-  s2 >>= 16;
-  return top > 0 ? top - 1 : nn;
-}
-
 // Threaded-BVH walk over the spheres (scenes with >= kBvhMinSpheres).  The
 // brute-force scan in index order with a strict '<' returns the
 // lexicographic minimum of (t, quads before spheres, sphere index); the walk
@@ -1104,9 +1044,6 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
   constexpr bool kWalk = kBvh;
   int wni = -1;                             // the path's next BVH node; -1: its quads are not scanned yet
   Hit wh{3.40282347e+38f, -1, 0};           // its closest hit so far
-#if RTP_BVH_PAIR
-  uint64_t pst0 = 0, pst1 = 0, pst2 = 0;  // the pair walk's stack (pair_visit)
-#endif
   Path ps;
   ps.org = eye;
   ps.dir = mk(0.f, 0.f, 1.f);
@@ -1330,20 +1267,10 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
     unsigned long long tbnc = ta;
     bool shade = has_path;
     if constexpr (kWalk) {
-#if RTP_BVH_PAIR
-      const bool pair_walk = !kLdsBvh && sc->n_pair > 0;  // (wave-uniform)
-      const int nn = pair_walk ? sc->n_pair : kLdsBvh ? sc->n_lw_nodes : sc->n_nodes;
-#else
       const int nn = kLdsBvh ? sc->n_lw_nodes : sc->n_nodes;
-#endif
       if (has_path && wni < 0) {  // a new ray: the quads first (their hit bounds the walk)
         wh = closest_hit<false, false>(sc, ps.org, ps.dir, true, nullptr, s_qshade + kPrexLdsOffset);
         wni = 0;
-#if RTP_BVH_PAIR
-        pst0 = 0;
-        pst1 = 0;
-        pst2 = 0;
-#endif
       }
       const uint64_t pm = __ballot(has_path);
       const int need = min(RTP_WALK_DONE, __popcll(pm));
@@ -1364,29 +1291,6 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
           else return R.nodes[i];
         };
         u4v v = u4v{0u, 0u, 0u, 0u};
-#if RTP_BVH_PAIR
-        if (pair_walk) {
-          GU4* const pnodes = (GU4*)sc->pair_nodes;
-          GF4* const psph = (GF4*)sc->pair_sph;
-          BvhRay RP = R;
-          RP.orig = (GI32*)sc->pair_sidx;
-          const float porg[3] = {sc->pair_org[0], sc->pair_org[1], sc->pair_org[2]};
-          const float pscl[3] = {sc->pair_scl[0], sc->pair_scl[1], sc->pair_scl[2]};
-          if (walking) v = pnodes[wni];
-          for (;;) {
-            const uint64_t wm = __ballot(walking);
-            if (wm == 0 || __popcll(pm & ~wm) >= need) break;
-            if (walking) {
-              const int next = pair_visit(psph, RP, porg, pscl, o, d, v, wh, pst0, pst1, pst2, nn);
-              walking = next < nn;
-              if (walking) v = pnodes[next];
-              wni = next;
-            }
-          }
-          if (has_path && !walking) bvh_resolve(wh, RP);
-        } else
-#endif
-        {
         if (walking) v = node(wni);
         for (;;) {
           const uint64_t wm = __ballot(walking);
@@ -1399,7 +1303,6 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
           }
         }
         if (has_path && !walking) bvh_resolve(wh, R);
-        }
       }
       shade = has_path && !walking;
       if (want_dbg) dbg[kDbgCyclesIntersect] += stamp(want_dbg) - ta;

@@ -223,16 +223,7 @@ struct alignas(16) DevScene {
   // bits left out of the mask order those axes' splits left child first
   // (fewer distinct copies: a smaller footprint in the texture cache)
   int32_t oct_mask;
-  // pair nodes (experiment, rtp_kernels.hip RTP_BVH_PAIR): one 16-byte record
-  // per inner node of the host-built tree with BOTH children's boxes, 8 bits
-  // per coordinate on the grid x = pair_org + q * pair_scl (rounded outward),
-  // and two 16-bit child references (bit 15: a sphere, index into pair_sph /
-  // pair_sidx; else a pair node); n_pair = 0: not built
-  int32_t n_pair;
-  float pair_org[3], pair_scl[3];
-  const uint32_t* pair_nodes;
-  const float* pair_sph;     // float4 (centre, r^2) per sphere in pair order
-  const int32_t* pair_sidx;  // its scene index
+  int32_t pad3[2];
 };
 // The pool kernel's scans prefetch up to two records past the last quad or
 // prefilter record; these must stay inside DevScene (values never used).
