@@ -1,26 +1,33 @@
 """Benchmark of the path-tracing hot path (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload auto|c2|c4] [--scaling strong|weak]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload auto|c2|c4|c5] [--scaling strong|weak]
 
 One step = one full render of the workload's frame.  On one GPU (no process
 group) the frame goes through the library's default contiguous launch
 (rtp_render_device over [0, nx*ny), like main.cc's render; --n1-launch tiles:
-the tile-deal instance the ranks of an N-GPU run use).
+the tile-deal instance the ranks of a tile-sharded run use).
   c2: Cornell Box 800x800, 1000 spp, depth 50 (BASELINE.json configs[1]), the
       metric's own image: the N = 1 workload (--workload auto).
   c4: Cornell Box 1920x1080, 4096 spp, depth 50 (BASELINE.json configs[3]),
-      the configuration BASELINE.json names for the 2/4/8-GPU image-tile
-      shard: the N > 1 workload (--workload auto).  On one GPU it renders at
-      the same rate as C2 (5591 vs 5646 Msamples/s, r03z2), so the driver's
-      N-GPU / 1-GPU ratio compares like with like.
+      image-tile shard over the ranks.
+  c5: Cornell Box 3840x2160, 16384 spp, depth 50 (BASELINE.json configs[4]),
+      sample-batch shard: the N > 1 workload (--workload auto).  Rank k renders
+      spp/N samples of EVERY pixel on its derived stream (seed = pixel + k*nx*ny,
+      shard.sample_batches), so no rank carries a whole pixel's sample chain
+      (the chain floor that caps the tile shards).
 N > 1 (launched by torch.distributed.run, one process per GPU):
-  --scaling strong (default): THE frame, its 16x16 tiles dealt to the ranks
-      round-robin; each rank renders 1/N of the pixels, and
-      the float4 framebuffer is summed to rank 0 with ONE reduce per step
-      (RCCL over xGMI), overlapped with the next step's render (two canvases,
-      alternating; exact: every pixel is non-zero on one rank).
+  --scaling strong (default): THE frame, split over the ranks (c2/c4: 16x16
+      tiles dealt round-robin; c5: sample batches); the float4
+      framebuffer is summed to rank 0 with ONE reduce per step (RCCL over xGMI),
+      overlapped with the next step's render (two canvases, alternating).
   --scaling weak: every rank renders a full nx x ny band of an nx x ny*N
       canvas (per-GPU work fixed).
+  After the timed region rank 0 renders the same workload's whole frame alone
+  (--anchor, default on): `one_gpu_same_workload` and
+  `speedup_vs_one_gpu_same_workload` compare like with like (the driver's
+  N-GPU / 1-GPU ratio divides C5's rate by C2's).  The N = 1 line carries
+  `scaling_anchors`: one-GPU kernel times of C4's whole frame and of one C5
+  rank share, measured in the same run.
 
 Rank 0 prints one JSON line.  `value` = all ranks' samples / max-over-ranks
 wall time of the K timed steps (steady state: the renderer's context, scene
@@ -28,11 +35,14 @@ and RNG jump tables are set up before the timed region -- `setup` and
 `first_render_ms` report what that costs, and `one_shot` what a fresh process
 rendering once, like main.cc, would see).  `rmse` / `bit_exact` compare the
 last timed frame (normalised, NormalizeFunctor) with the oracle's committed
-C2 frame (tests/golden/c2_full.npz).  `roofline` prices the render kernel with
-the SoA byte model of SURVEY.md 8(d) (56 + 88*L bytes per sample) against the
-8 TB/s HBM peak; `roofline_valu` gives the VALU-issue bound from the
-committed PMC summary; `cpu_baseline` times the oracle's stage-structured
-restatement on a bounded sample of the same workload on this host.
+C2 frame (tests/golden/c2_full.npz); C5 checks a rank's shard against the
+committed c5_shard3_2048spp fixture (bit-exact) and the reduced frame against
+the single-stream image statistically.  `roofline` prices the render kernel
+with the SoA byte model of SURVEY.md 8(d) (56 + 88*L bytes per sample) against
+the 8 TB/s HBM peak; `roofline_valu` gives the VALU-issue bound (the one that
+binds) from the committed PMC summary; `cpu_baseline` times
+the oracle's stage-structured restatement on a bounded sample of the same
+workload on this host.
 """
 from __future__ import annotations
 
@@ -56,7 +66,12 @@ WORKLOADS = {
            "name": "C2: Cornell Box 800x800, 1000 spp, depth 50"},
     "c4": {"nx": 1920, "ny": 1080, "spp": 4096, "depth": 50, "golden": "c4_subset16k.npz",
            "name": "C4: Cornell Box 1920x1080, 4096 spp, depth 50 (BASELINE configs[3], image-tile shard)"},
+    "c5": {"nx": 3840, "ny": 2160, "spp": 16384, "depth": 50, "golden": "c5_shard3_2048spp.npz",
+           "name": "C5: Cornell Box 3840x2160, 16384 spp, depth 50 (BASELINE configs[4], sample-batch shard)"},
 }
+SHARD = {"c2": "tiles", "c4": "tiles", "c5": "samples"}
+# pixels of the C5 frame compared with the single-stream image (statistical check)
+C5_CHECK_PIXELS = 65536
 
 
 def cpu_baseline(budget_s: float, nx: int, ny: int, depth: int, nthreads: int = 1) -> dict:
@@ -115,7 +130,7 @@ def load_traffic(path: str, cfg: dict):
     return None
 
 
-def load_golden_frame(path: str):
+def load_golden_frame(path: str, any_seed: bool = False):
     """The oracle's committed fixture of the workload: tests/golden/c2_full.npz
     (tools/make_golden.py full_frame_fixture, every pixel: un-normalised rgb
     sums [N, 3]) or a pixel-subset fixture (c4_subset16k.npz: `pixels` and
@@ -128,10 +143,10 @@ def load_golden_frame(path: str):
         rgb, pixels = np.ascontiguousarray(z["rgb_planes"].T).view(np.float32).reshape(-1, 3), None
     else:
         rgb, pixels = np.asarray(z["rgb"], np.float32), np.asarray(z["pixels"], np.int64)
-        if int(z["seed_base"]) != 0:
+        if int(z["seed_base"]) != 0 and not any_seed:
             return None
     return {"rgb": rgb, "pixels": pixels, "nx": int(z["nx"]), "ny": int(z["ny"]), "spp": int(z["spp"]),
-            "depth": int(z["depth"])}
+            "depth": int(z["depth"]), "seed_base": int(z["seed_base"]) if "seed_base" in z.files else 0}
 
 
 def frame_quality(canvas: np.ndarray, gold: dict, spp: int) -> dict:
@@ -167,10 +182,57 @@ def load_valu(path: str, cfg: dict, kernel_ms: float):
         return None
     cap = t["simds"] * t["gpu_cycles_per_launch"] / t["cycles_per_wave64_valu"]
     frac = t["valu_insts_per_launch"] / cap
+    lanes = t.get("lanes_per_instr")
     return {"bound": "valu-issue", "achieved": t["valu_insts_per_launch"] / (kernel_ms / 1e3) / 1e12,
             "peak": t["simds"] * t["clock_ghz"] * 1e9 / t["cycles_per_wave64_valu"] / 1e12,
             "unit": "T wave64-VALU instr/s", "frac": round(frac, 4),
-            "lanes_per_instr": t.get("lanes_per_instr"), "source": t.get("source")}
+            "lanes_per_instr": lanes,
+            # issue slots x the fraction of their 64 lanes doing work: the
+            # lane-weighted VALU utilisation
+            "lane_frac": None if lanes is None else round(frac * lanes / 64.0, 4),
+            "source": t.get("source")}
+
+
+def timed_ms(fn) -> float:
+    """Kernel time of one render (rtp_stats.kernel_ms: HIP events on the
+    launch's stream, synchronised)."""
+    return float(fn().kernel_ms)
+
+
+def scaling_anchors(dev, cam, stream) -> dict:
+    """One-GPU kernel times of the multi-GPU workloads, on this GPU in this
+    run: C4's whole frame through the tile instance its ranks use, and one
+    rank's share of the C5 frame at N = 8 (2048 of 16384 spp on its derived
+    stream), so that an N-GPU line of either workload can be read against
+    the same workload on one GPU."""
+    import torch
+
+    out = {}
+    c4 = WORKLOADS["c4"]
+    n_tiles = -(-c4["nx"] // TILE) * -(-c4["ny"] // TILE)
+    buf = torch.empty((TILE * TILE * n_tiles, 4), dtype=torch.float32, device="cuda")
+    ms = timed_ms(lambda: dev.render_tiles_device(cam, c4["nx"], c4["ny"], c4["spp"], c4["depth"], buf.data_ptr(), 0, 1,
+                                                  stream=stream, timed=True))
+    smp = c4["nx"] * c4["ny"] * c4["spp"]
+    out["c4_whole_frame"] = {"config": "1920x1080, 4096 spp, depth 50", "kernel_ms": round(ms, 2),
+                             "msamples_per_s": round(smp / ms / 1e3, 1),
+                             "launch": "tile instance, rank 0 of 1 (the instance every rank of a C4 run launches)"}
+    del buf
+    c5 = WORKLOADS["c5"]
+    npix = c5["nx"] * c5["ny"]
+    from raytracingtherestofyourlife_amd import shard
+
+    b = shard.sample_batches(c5["spp"], 8, npix)[0]
+    buf = torch.empty((npix, 4), dtype=torch.float32, device="cuda")
+    ms = timed_ms(lambda: dev.render_device(cam, c5["nx"], c5["ny"], b.spp, c5["depth"], buf.data_ptr(),
+                                            seed_base=b.seed_base, stream=stream, timed=True))
+    out["c5_share_of_8"] = {"config": f"3840x2160, {b.spp} of 16384 spp (rank 0 of 8), depth 50",
+                            "kernel_ms": round(ms, 2), "msamples_per_s": round(npix * b.spp / ms / 1e3, 1),
+                            "one_gpu_frame_ms_est": round(8 * ms, 1),
+                            "launch": "contiguous pixels, work stealing (the instance every rank of a C5 run launches)"}
+    del buf
+    torch.cuda.synchronize()
+    return out
 
 
 def main() -> None:
@@ -179,9 +241,10 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
-                    help="strong: the one 800x800 frame dealt over the ranks; weak: an 800x800 band per rank")
-    ap.add_argument("--workload", default="auto", choices=["auto", "c2", "c4"],
-                    help="auto: c2 on one GPU (the metric's frame), c4 on N > 1 (the tile-shard configuration)")
+                    help="strong: the one frame split over the ranks (tiles or sample batches); weak: a band per rank")
+    ap.add_argument("--workload", default="auto", choices=["auto", "c2", "c4", "c5"],
+                    help="auto: c2 on one GPU (the metric's frame), c5 on N > 1 (the sample-batch shard "
+                         "configuration)")
     ap.add_argument("--nx", type=int, default=None, help="override the workload's width")
     ap.add_argument("--ny", type=int, default=None, help="rows of the frame (weak: per GPU, canvas nx x ny*N)")
     ap.add_argument("--spp", type=int, default=None)
@@ -194,13 +257,22 @@ def main() -> None:
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL over xGMI, production); gloo: host-side reduce, for rehearsing N>1 on one GPU")
     ap.add_argument("--share-gpu", action="store_true", help="every rank uses device 0 (rehearsal on a 1-GPU box)")
-    ap.add_argument("--check", action="store_true", help="rank 0 verifies the reduced canvas against a 1-process render")
+    ap.add_argument("--check", action="store_true",
+                    help="rank 0 verifies the reduced canvas against its own one-GPU render of the frame "
+                         "(implied by --anchor on a process group)")
+    ap.add_argument("--anchor", default="on", choices=["on", "off"],
+                    help="process group: rank 0 renders the same workload's whole frame alone after the timed "
+                         "region (one_gpu_same_workload, speedup_vs_one_gpu_same_workload, the checks)")
+    ap.add_argument("--scaling-anchors", default="auto", choices=["auto", "on", "off"],
+                    help="N = 1: time C4's whole frame and one C5 rank share on this GPU (auto: on for the "
+                         "default c2 workload at its own size)")
     ap.add_argument("--force-collective", action="store_true",
                     help="create the process group and run the per-step reduce even on one rank (torchrun "
                          "--nproc-per-node 1: exercises the RCCL path on a one-GPU box)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c2.json"))
     ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "valu_c2.json"))
-    ap.add_argument("--golden", default=None, help="whole-frame fixture (c2) or pixel-subset fixture (c4)")
+    ap.add_argument("--golden", default=None, help="whole-frame fixture (c2), pixel-subset fixture (c4) or a "
+                                                   "sample-shard fixture (c5)")
     ap.add_argument("--n1-launch", default="contig", choices=["contig", "tiles"],
                     help="one GPU, no process group: contig = the whole frame through the library's default launch "
                          "(rtp_render_device over [0, nx*ny), like main.cc's render); tiles = the tile-deal instance "
@@ -218,8 +290,9 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    workload = args.workload if args.workload != "auto" else ("c2" if world == 1 else "c4")
+    workload = args.workload if args.workload != "auto" else ("c2" if world == 1 else "c5")
     W = WORKLOADS[workload]
+    sized = all(getattr(args, k) is None for k in ("nx", "ny", "spp", "depth"))
     for k in ("nx", "ny", "spp", "depth"):
         if getattr(args, k) is None:
             setattr(args, k, W[k])
@@ -238,9 +311,16 @@ def main() -> None:
     nx, ny = args.nx, args.ny * (1 if strong else world)
     # one GPU without a process group renders the frame in pixel order through
     # the default contiguous launch (--n1-launch contig); ranks of a group
-    # render their tiles
+    # render their tiles (c2, c4, weak bands) or their sample batch (c5)
     contig = world == 1 and not (args.force_collective) and args.n1_launch == "contig"
-    ids_np = np.arange(nx * ny, dtype=np.int64) if contig else shard.tile_pixels(nx, ny, rank, world)
+    mode = "contig" if contig else (SHARD[workload] if strong else "tiles")
+    samples = mode == "samples"
+    spp_mine, seed_base = args.spp, 0
+    if samples:
+        b = shard.sample_batches(args.spp, world, nx * ny)[rank]
+        spp_mine, seed_base = b.spp, b.seed_base
+    ids_np = np.arange(nx * ny, dtype=np.int64) if mode in ("contig", "samples") else shard.tile_pixels(nx, ny, rank,
+                                                                                                         world)
     npix = ids_np.size
     # setup, timed: the context, the scene, the RNG jump tables (policy), then
     # the first render -- what a fresh process pays before its first frame.
@@ -257,7 +337,7 @@ def main() -> None:
     ff = dev.set_ff_tables(args.ff_tables)
     t_ff = time.perf_counter()
     cam = rtp.default_camera()
-    ids = torch.from_numpy(ids_np).cuda()
+    ids = None if mode in ("contig", "samples") else torch.from_numpy(ids_np).cuda()
     out = torch.empty((npix, 4), dtype=torch.float32, device="cuda")
     canvas = torch.zeros((nx * ny, 4), dtype=torch.float32, device="cuda")
     live = torch.zeros(npix, dtype=torch.int32, device="cuda")
@@ -273,7 +353,7 @@ def main() -> None:
     # renders clipped edge tiles whole (C4's 1080 rows: 0.7% more work, not
     # counted as samples): the entries inside the canvas are scattered
     # (shard.tile_entries).  RTP_BENCH_LIST=1: the explicit pixel list.
-    tiled = (not contig) and os.environ.get("RTP_BENCH_LIST") != "1"
+    tiled = mode == "tiles" and os.environ.get("RTP_BENCH_LIST") != "1"
     if tiled:
         ent_np, pix_np = shard.tile_entries(nx, ny, rank, world)
         assert np.array_equal(pix_np, ids_np)
@@ -291,21 +371,19 @@ def main() -> None:
         red.drain()
 
     def render():
-        if contig:
-            dev.render_device(cam, nx, ny, args.spp, args.depth, out.data_ptr(), pixel_count=npix,
-                              stream=stream.cuda_stream)
-        elif tiled:
+        if tiled:
             dev.render_tiles_device(cam, nx, ny, args.spp, args.depth, tile_out.data_ptr(), rank, world,
                                     stream=stream.cuda_stream)
-        else:
-            dev.render_device(cam, nx, ny, args.spp, args.depth, out.data_ptr(), pixel_count=npix,
-                              pixel_ids_ptr=ids.data_ptr(), stream=stream.cuda_stream)
+        else:  # contiguous pixels (the whole frame, or a sample batch of it), or the pixel list
+            dev.render_device(cam, nx, ny, spp_mine, args.depth, out.data_ptr(), pixel_count=npix,
+                              pixel_ids_ptr=0 if ids is None else ids.data_ptr(), seed_base=seed_base,
+                              stream=stream.cuda_stream)
 
     def step(count_live: bool = False):
-        if count_live:  # (the list path carries the per-pixel live-bounce counters)
-            dev.render_device(cam, nx, ny, args.spp, args.depth, out.data_ptr(), pixel_count=npix,
-                              pixel_ids_ptr=0 if contig else ids.data_ptr(), stream=stream.cuda_stream,
-                              live_ptr=live.data_ptr())
+        if count_live:  # (the list / contiguous path carries the per-pixel live-bounce counters)
+            dev.render_device(cam, nx, ny, spp_mine, args.depth, out.data_ptr(), pixel_count=npix,
+                              pixel_ids_ptr=0 if ids is None else ids.data_ptr(), seed_base=seed_base,
+                              stream=stream.cuda_stream, live_ptr=live.data_ptr())
             return red.step(ids, out)
         render()
         return gather_canvas()
@@ -339,15 +417,89 @@ def main() -> None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if args.steps else float("nan")
+
+    # ---- after the timed region: checks and the same-workload one-GPU anchor ----
+    coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
+    quality = None
+    shard_exact = None
+    gathered = None
+    if samples:
+        # (a) a rank whose batch is a committed fixture's (c5_shard3_2048spp:
+        # rank 3 of 8) compares its own last shard with it, bit for bit
+        code = torch.tensor([-1], dtype=torch.int64)
+        g = load_golden_frame(args.golden, any_seed=True)
+        if g and g["pixels"] is not None and (g["nx"], g["ny"], g["spp"], g["depth"], g["seed_base"]) == (
+                nx, ny, spp_mine, args.depth, seed_base):
+            part = out.index_select(0, torch.from_numpy(g["pixels"]).cuda())[:, :3].cpu().numpy()
+            same = (part.view(np.uint32) == g["rgb"].view(np.uint32)) | (np.isnan(part) & np.isnan(g["rgb"]))
+            code[0] = 1 if same.all() else 0
+        codes = [torch.zeros(1, dtype=torch.int64, device=coll_dev) for _ in range(world)]
+        if grouped:
+            dist.all_gather(codes, code.to(coll_dev))
+        else:
+            codes = [code]
+        hit = [r for r in range(world) if int(codes[r].item()) >= 0]
+        if hit:
+            shard_exact = {"fixture": os.path.basename(args.golden), "rank": hit[0],
+                           "pixels": int(g["rgb"].shape[0]) if g else None,
+                           "bit_exact": all(int(codes[r].item()) == 1 for r in hit)}
+        # (b) every rank's shard at a fixed pixel sample, gathered to rank 0
+        # for the statistical comparison with the single-stream image
+        chk = np.sort(np.random.default_rng(5).choice(nx * ny, min(C5_CHECK_PIXELS, nx * ny), replace=False))
+        mine = out.index_select(0, torch.from_numpy(chk).cuda()).to(coll_dev)
+        if grouped and world > 1:
+            parts = [torch.empty_like(mine) for _ in range(world)]
+            dist.all_gather(parts, mine)
+            gathered = [q.cpu().numpy() for q in parts]
+        else:
+            gathered = [mine.cpu().numpy()]
+
+    one_gpu = None
     check = None
-    if args.check and rank == 0:
-        # the reduced canvas must equal one process rendering every pixel (bit-exact, NaN-aware)
+    want_anchor = grouped and args.anchor == "on"
+    if rank == 0 and (want_anchor or args.check):
+        # rank 0 renders the same workload's whole frame alone: the one-GPU
+        # time of this workload (the others wait at the barrier below)
         full = torch.empty((nx * ny, 4), dtype=torch.float32, device="cuda")
-        dev.render_device(cam, nx, ny, args.spp, args.depth, full.data_ptr(), stream=stream.cuda_stream)
+        st = dev.render_device(cam, nx, ny, args.spp, args.depth, full.data_ptr(), stream=stream.cuda_stream,
+                               timed=True)
         torch.cuda.synchronize()
-        a, b = canvas[:, :3].cpu().numpy(), full[:, :3].cpu().numpy()
-        same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
-        check = bool(same.all())
+        one_ms = float(st.kernel_ms)
+        one_gpu = {"kernel_ms": round(one_ms, 2),
+                   "msamples_per_s": round(nx * ny * args.spp / one_ms / 1e3, 1),
+                   "launch": "rank 0's GPU alone, the whole frame through the default contiguous launch"
+                             + (" on the single stream (seed_base 0: the N = 1 schedule; same pixels, samples "
+                                "and scene as the sharded frame)" if samples else "")}
+        red_np = canvas[:, :3].cpu().numpy()
+        if samples:
+            single = full.index_select(0, torch.from_numpy(chk).cuda()).cpu().numpy()
+            # the shards summed in rank order in float32 (a reduce of two ranks is one add: exact;
+            # more ranks may associate differently)
+            summed = gathered[0][:, :3].copy()
+            for q in gathered[1:]:
+                summed = summed + q[:, :3]
+            summed = summed.astype(np.float64)
+            red_chk = red_np[chk].astype(np.float64)
+            # the reduced frame against the single-stream image (shard.sample_shard_ttest: block means of the
+            # per-pixel difference, Student-t); both estimate the same radiance
+            stats = shard.sample_shard_ttest(single, red_chk, args.spp)
+            fin = np.isfinite(summed) & np.isfinite(red_chk)
+            rel = float(np.max(np.abs(red_chk[fin] - summed[fin]) / np.maximum(np.abs(summed[fin]), 1e-30))) \
+                if fin.any() else 0.0
+            check = {"pixels": int(chk.size),
+                     "reduced_equals_sum_of_shards_max_rel": rel,
+                     "nan_pattern_equal": bool(np.array_equal(np.isnan(red_chk), np.isnan(summed))),
+                     "statistics_vs_single_stream": stats,
+                     "consistent": shard.ttest_consistent(stats)}
+        else:
+            # the reduced canvas must equal one process rendering every pixel (bit-exact, NaN-aware)
+            b_np = full[:, :3].cpu().numpy()
+            same = (red_np.view(np.uint32) == b_np.view(np.uint32)) | (np.isnan(red_np) & np.isnan(b_np))
+            check = bool(same.all())
+        del full
+    if grouped:
+        dist.barrier()
+
     # a one-shot render on the library's default policy (AUTO: no jump tables
     # for a single C2 frame), as main.cc's rtp_render would run it: the whole
     # frame, tables switched off (one process: N = 1 only).  It runs through
@@ -370,14 +522,16 @@ def main() -> None:
         off_ms = (time.perf_counter() - t_off) * 1e3
         del full_off
         dev.set_ff_tables(args.ff_tables)
-    quality = None
-    if rank == 0:
+    anchors = None
+    if world == 1 and not grouped and (args.scaling_anchors == "on" or (
+            args.scaling_anchors == "auto" and workload == "c2" and sized)):
+        anchors = scaling_anchors(dev, cam, stream.cuda_stream)
+    if rank == 0 and not samples:
         gold = load_golden_frame(args.golden)
         if gold and (gold["nx"], gold["ny"], gold["spp"], gold["depth"]) == (nx, ny, args.spp, args.depth):
             quality = frame_quality(canvas.cpu().numpy(), gold, args.spp)
     if grouped:
-        t = torch.tensor([elapsed, live_total], dtype=torch.float64,
-                         device="cuda" if args.dist_backend == "nccl" else "cpu")
+        t = torch.tensor([elapsed, live_total], dtype=torch.float64, device=coll_dev)
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         tot = t.clone()
@@ -387,7 +541,7 @@ def main() -> None:
     else:
         live_all = float(live_total)
 
-    samples_rank = npix * args.spp
+    samples_rank = npix * spp_mine
     samples_all = nx * ny * args.spp
     value = samples_all * args.steps / elapsed / 1e6
     L = live_all / samples_all
@@ -403,7 +557,10 @@ def main() -> None:
         "ff_tables": {k: ff[k] for k in ("policy", "built", "chain_tables", "direct_first", "direct_count")}
                      | {"gib": round(ff["bytes"] / 2**30, 1), "alloc_ms": round(ff["alloc_ms"], 1),
                         "build_ms": round(ff["build_ms"], 1),
-                        "render_ms_without": round(off_ms, 2) if world == 1 else None},
+                        "render_ms_without": round(off_ms, 2) if world == 1 else None,
+                        "per_rank": (f"every rank builds its own tables on its own GPU before its first frame "
+                                     f"({round(ff['bytes'] / 2**30, 1)} GiB of each GPU's HBM; this line: rank 0's "
+                                     f"setup)") if grouped else None},
     }
     first_ms = (t_first_done - t_first) * 1e3
     setup_base_ms = (t_scene - t_setup) * 1e3  # context + scene
@@ -415,13 +572,18 @@ def main() -> None:
             cpu = cpu_baseline(args.cpu_budget, args.nx, args.ny, args.depth)
         if world == 1 and args.cpu_budget_mt > 0:
             cpu_mt = cpu_baseline(args.cpu_budget_mt, args.nx, args.ny, args.depth, nthreads=host_threads())
+        backend = "RCCL" if args.dist_backend == "nccl" else "gloo"
         if contig:
             shard_desc = "one GPU: the whole frame in pixel order (the default contiguous launch)"
         elif world == 1 and not grouped:
             shard_desc = "one GPU: the whole frame"
+        elif samples:
+            shard_desc = (f"sample batches: rank k renders spp/{world} samples of every pixel on the derived stream "
+                          f"seed = pixel + k*{nx * ny} (shard.sample_batches), 1 {backend} reduce/step")
         else:
-            shard_desc = (f"{TILE}x{TILE} tiles round-robin over {world} rank(s), 1 "
-                          + ("RCCL" if args.dist_backend == "nccl" else "gloo") + " reduce/step")
+            shard_desc = (f"{TILE}x{TILE} tiles round-robin over {world} rank(s), 1 {backend} reduce/step"
+                          + (" (pixel of each tile entry computed in-kernel)" if tiled else " (pixel list)"))
+        ms_step = elapsed / max(args.steps, 1) * 1e3
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -429,19 +591,19 @@ def main() -> None:
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / max(args.steps, 1) * 1e3, 3),
+            "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32 (f64 mixture/pdf islands)",
             "data": "synthetic: the reference's deterministic Cornell Box scene and camera (main.cc:616-622), "
-                    "seed = pixel index",
+                    "seed = pixel index" + (" + k*nx*ny on rank k (sample batches)" if samples else ""),
             "config": {
                 "workload": W["name"] + ("" if strong or world == 1 else f" per GPU (canvas {nx}x{ny})"),
                 "nx": nx, "ny": ny, "spp": args.spp, "depth": args.depth,
                 "pixels_per_gpu": npix,
-                "shard": shard_desc + ("" if contig else " (pixel of each tile entry computed in-kernel)" if tiled
-                                       else " (pixel list)"),
+                "spp_per_gpu": spp_mine,
+                "shard": shard_desc,
                 "live_bounces_per_sample": round(L, 6),
                 "dist_backend": args.dist_backend if grouped else None,
             },
@@ -476,8 +638,15 @@ def main() -> None:
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_mt,
         }
+        if anchors is not None:
+            line["scaling_anchors"] = anchors
+        if one_gpu is not None:
+            line["one_gpu_same_workload"] = one_gpu
+            line["speedup_vs_one_gpu_same_workload"] = round(one_gpu["kernel_ms"] / ms_step, 3)
+        if shard_exact is not None:
+            line["shard_exact"] = shard_exact
         if check is not None:
-            line["check_reduced_canvas_equals_single_render"] = check
+            line["check_reduced_canvas" + ("" if samples else "_equals_single_render")] = check
         print(json.dumps(line), flush=True)
     if grouped:
         dist.destroy_process_group()

@@ -153,7 +153,11 @@ rtp_status rtp_render_device(rtp_context* ctx, const rtp_camera* cam, int32_t nx
  * int32[n_waves+1], non-decreasing, ending at pixel_count).  Grouping pixels
  * of similar cost into the same wave keeps its lanes busy to the end (a
  * pixel's samples are one sequential chain).  Results are identical to
- * rtp_render_device for any plan.  Scenes without the sphere BVH only. */
+ * rtp_render_device for any plan.  Scenes without the sphere BVH only.
+ * NOT asynchronous like rtp_render_device: the plan is copied to the host and
+ * validated before the launch, which waits for the work already queued on
+ * hip_stream (an experiment's entry point: a bad plan is an error, not a
+ * silently clamped launch). */
 rtp_status rtp_render_planned_device(rtp_context* ctx, const rtp_camera* cam, int32_t nx, int32_t ny, int32_t spp,
                                      int32_t depth, uint32_t seed_base, int64_t pixel_begin, int64_t pixel_count,
                                      const int64_t* d_pixel_ids, const int32_t* d_wave_begin, int32_t n_waves,
@@ -308,6 +312,12 @@ rtp_status rtp_debug_closest_hit(rtp_context* ctx, const float* rays, int64_t n,
  * RTP_BVH_LDS=1 at rtp_set_scene, and only when its nodes and spheres fit the
  * LDS). */
 int32_t rtp_sphere_walk(rtp_context* ctx);
+
+/* Diagnostics: the octant mask of the current scene's global sphere walk (a
+ * ray in direction octant o walks the near-to-far copy o & mask; 7: all 8
+ * copies, the default for the host SAH and the device LBVH builds alike;
+ * RTP_BVH_OCT_MASK narrows it for experiments); -1 without a sphere BVH. */
+int32_t rtp_sphere_walk_oct_mask(rtp_context* ctx);
 
 /* Diagnostics: exhaustively compare a fast device arithmetic sequence with the
  * IEEE operation for every float bit pattern in [lo_bits, hi_bits].  kind 0:

@@ -74,7 +74,7 @@ EXPORTED_SYMBOLS = [
     "rtp_eval_primitive", "rtp_debug_counters", "rtp_verify_fast_math", "rtp_debug_closest_hit",
     "rtp_render_direct", "rtp_render_direct_device", "rtp_sample_color_table", "rtp_quad_scalars",
     "rtp_cornell_point_field", "rtp_write_pnm_depth", "rtp_eval_powf", "rtp_set_ff_tables", "rtp_get_ff_tables",
-    "rtp_render_planned_device", "rtp_sphere_walk",
+    "rtp_render_planned_device", "rtp_sphere_walk", "rtp_sphere_walk_oct_mask",
 ]
 
 
@@ -152,6 +152,7 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.rtp_set_ff_tables.argtypes = [vp, ctypes.c_int32]
     L.rtp_get_ff_tables.argtypes = [vp, ctypes.POINTER(RtpFfInfo)]
     L.rtp_sphere_walk.argtypes = [vp]
+    L.rtp_sphere_walk_oct_mask.argtypes = [vp]
     for name in EXPORTED_SYMBOLS:
         if name not in ("rtp_last_error", "rtp_abi_version", "rtp_destroy"):
             getattr(L, name).restype = ctypes.c_int32

@@ -33,6 +33,7 @@ struct rtp_context {
   int32_t* d_lw_orig = nullptr;
   int lw_bytes = 0;  // its LDS footprint (0: the scene has no LDS walk)
   bool use_bvh = false;
+  int oct_mask = 0;  // the global walk's octant mask (DevScene::oct_mask) of the current scene
   int ff_policy = 0;  // rtp_ff_policy (RNG jump tables)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // Completion of the last launch.  The history buffer and the progress

@@ -629,8 +629,10 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     return t >= 0 && t < s->n_tex_type && s->tex_type[t] >= 0 && s->tex_type[t] < s->n_tex;
   };
   rtp::DevScene* h = new rtp::DevScene();
-  h->oct_mask = 7;  // (every octant its own walk order; the host SAH build may narrow it)
   std::memset(h, 0, sizeof(*h));
+  // (after the memset: every octant its own walk order -- the device LBVH
+  // build keeps all 8; the host SAH build may narrow it, RTP_BVH_OCT_MASK)
+  h->oct_mask = 7;
   std::vector<int> kept;
   std::vector<rtp::DevQuad> built;
   for (int q = 0; q < s->n_quads; q++) {
@@ -943,6 +945,7 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
   c->lw_bytes = h->n_lw_nodes > 0 ? 16 * (8 * h->n_lw_nodes + h->n_lw_sph) : 0;
   delete h;
   c->use_bvh = use_bvh;
+  c->oct_mask = use_bvh ? h->oct_mask : 0;
   if (e != hipSuccess) return hip_fail(e, "rtp_set_scene upload");
   c->kept_quads = std::move(kept_ref);
   c->n_ref_quads = s->n_quads;
@@ -1334,6 +1337,11 @@ rtp_status rtp_debug_closest_hit(rtp_context* c, const float* rays, int64_t n, u
 int32_t rtp_sphere_walk(rtp_context* c) {
   if (!c || !c->has_scene || !c->use_bvh) return 0;
   return c->lw_bytes > 0 ? 2 : 1;
+}
+
+int32_t rtp_sphere_walk_oct_mask(rtp_context* c) {
+  if (!c || !c->has_scene || !c->use_bvh) return -1;
+  return c->oct_mask;
 }
 
 // Diagnostics: exhaustive device check of a fast arithmetic sequence (kind,

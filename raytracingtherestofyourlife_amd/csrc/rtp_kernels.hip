@@ -1311,7 +1311,8 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
       f3 emit = mk(0.f, 0.f, 0.f);
       int res;
       if constexpr (kWalk) {
-        res = shade_hit<kBvh, true>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D, s_qshade, wh);
+        res = shade_hit<kBvh, true>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D, s_qshade, wh,
+                                    gdbg);  // (stats build: the region counters; nullptr otherwise)
         wni = -1;
       } else {
         res = bounce<kBvh, true>(sc, ps, seed, emit, hist + (int64_t)ps.d * stride, D, want_dbg ? dbg : nullptr,

@@ -348,6 +348,12 @@ class Device:
         'lds' (the LDS-resident walk)."""
         return ("scan", "global", "lds")[self._L.rtp_sphere_walk(self.handle)]
 
+    def sphere_walk_oct_mask(self) -> int:
+        """The global sphere walk's octant mask (rtp_sphere_walk_oct_mask): 7
+        = every direction octant walks its own near-to-far copy; -1 without a
+        sphere BVH."""
+        return int(self._L.rtp_sphere_walk_oct_mask(self.handle))
+
     def set_ff_tables(self, policy: str) -> dict:
         """RNG jump-table policy of this context (include/rtp.h rtp_set_ff_tables):
         'auto' (default), 'off', or 'on' (build now: a long-lived renderer).

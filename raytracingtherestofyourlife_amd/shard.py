@@ -131,16 +131,21 @@ class OverlappedCanvasReduce:
         self.steps = 0
 
     def step(self, ids, part):
-        """Zero the next canvas, scatter `part` at `ids`, start its reduce;
-        returns that canvas (rank 0 holds the sum once drained)."""
+        """Zero the next canvas, scatter `part` at `ids` (ids None: `part` is
+        a whole canvas -- a sample batch of every pixel -- and is copied),
+        start its reduce; returns that canvas (rank 0 holds the sum once
+        drained)."""
         slot = self.steps % len(self.canvases)
         self.steps += 1
         if self.pending[slot] is not None:
             self.pending[slot].wait()
             self.pending[slot] = None
         c = self.canvases[slot]
-        c.zero_()
-        c.index_copy_(0, ids, part)
+        if ids is None:
+            c.copy_(part)
+        else:
+            c.zero_()
+            c.index_copy_(0, ids, part)
         if self.collective:
             if len(self.canvases) > 1:
                 self.pending[slot] = self.dist.reduce(c, dst=0, op=self.dist.ReduceOp.SUM, async_op=True)
@@ -158,6 +163,97 @@ class OverlappedCanvasReduce:
             if w is not None:
                 w.wait()
                 self.pending[i] = None
+
+
+def sample_shard_consistency(single: np.ndarray, shards: list, spp: int) -> dict:
+    """Monte Carlo consistency of a sample-sharded image with the single-stream
+    image of the same frame (SURVEY.md 8(e) C5 "statistical vs the unsharded
+    reference"; shard.sample_batches).  single: the float32 [n, 4] sums of spp
+    samples per pixel on the reference's stream (seed_base 0); shards: G
+    arrays, each the sums of spp/G samples on its derived stream (seed_base
+    k*n).  The two images are two independent estimates of each pixel's mean
+    radiance, so their per-pixel difference D = (single - sum(shards)) / spp
+    has mean 0 and variance 2 sigma^2 / spp, with sigma^2 the per-sample
+    variance.  sigma^2 / (spp/G) is estimated per pixel from the spread of
+    the G shard means (ddof 1), so Var(D) ~ 2 s^2 / G.  Pixels that are NaN in
+    either image (a non-finite attenuation: the sum stays NaN, MapperPathTracer
+    .cxx:350; NormalizeFunctor zeroes it) are counted, not compared.
+    Returns: n (pixels compared), z_total (sum D / sqrt(sum Var D): ~N(0,1)),
+    ratio (sum D^2 / sum Var D: ~1), outliers (fraction with |D| > 5 sd),
+    norm_ratio (the same ratio after NormalizeFunctor, delta method:
+    Var(sqrt m) ~ Var(m) / (4 m)), nan_single / nan_sharded."""
+    G = len(shards)
+    x = np.asarray(single, np.float64)[:, :3]
+    ys = np.stack([np.asarray(s, np.float64)[:, :3] for s in shards])  # [G, n, 3]
+    nan = np.isnan(x).any(1) | np.isnan(ys).any((0, 2))
+    keep = ~nan
+    x, ys = x[keep], ys[:, keep]
+    mx = x / spp
+    my = ys.sum(0) / spp
+    means = ys / (spp / G)  # per-shard means
+    var_d = 2.0 * means.var(0, ddof=1) / G  # [n, 3]
+    d = mx - my
+    live = var_d > 0
+    z = np.zeros_like(d)
+    z[live] = d[live] / np.sqrt(var_d[live])
+    m = np.maximum(0.5 * (mx + my), 1e-12)
+    nx_, ny_ = np.sqrt(mx), np.sqrt(my)
+    return {
+        "n": int(keep.sum()),
+        "z_total": float(d[live].sum() / np.sqrt(var_d[live].sum())),
+        "ratio": float((d[live] ** 2).sum() / var_d[live].sum()),
+        "outliers": float((np.abs(z) > 5).mean()),
+        "zero_var_nonzero_d": int(((~live) & (d != 0)).sum()),
+        "norm_ratio": float(((nx_ - ny_)[live] ** 2).sum() / (var_d[live] / (4 * m[live])).sum()),
+        "nan_single": int(np.isnan(np.asarray(single)[:, :3]).any(1).sum()),
+        "nan_sharded": int(np.isnan(np.stack([np.asarray(s)[:, :3] for s in shards])).any((0, 2)).sum()),
+    }
+
+
+
+def sample_shard_ttest(single: np.ndarray, shards_sum: np.ndarray, spp: int, blocks: int = 256) -> dict:
+    """Frame-level test that a sample-sharded image (shards_sum: the G shards'
+    sums, spp samples per pixel in all) and the single-stream image of the
+    same pixels estimate the same radiance, with no per-pixel variance
+    estimate (the per-pixel one of sample_shard_consistency is unstable when
+    few shards hold a rare light hit).  The pixels (in the given order) are
+    cut into `blocks` groups; each group's mean difference of the per-pixel
+    means is an independent, near-Gaussian draw with mean 0 under the null, so
+    t = mean / (sd / sqrt(blocks)) per channel is Student-t with blocks - 1
+    degrees of freedom.  Pixels NaN in either image are left out (counted).
+    Returns t per channel, max |t|, the relative difference of the frame means
+    per channel, and the counts."""
+    x = np.asarray(single, np.float64)[:, :3] / spp
+    y = np.asarray(shards_sum, np.float64)[:, :3] / spp
+    keep = ~(np.isnan(x).any(1) | np.isnan(y).any(1))
+    d = (x - y)[keep]
+    B = max(2, min(blocks, d.shape[0] // 2))
+    m = np.stack([g.mean(0) for g in np.array_split(d, B)])  # [B, 3]
+    sd = m.std(0, ddof=1)
+    t = np.where(sd > 0, m.mean(0) / np.where(sd > 0, sd, 1.0) * np.sqrt(B), 0.0)
+    mx = x[keep].mean(0)
+    rel = np.where(mx != 0, (y[keep].mean(0) - mx) / np.where(mx != 0, mx, 1.0), 0.0)
+    return {"n": int(keep.sum()), "blocks": int(B), "t": [round(float(v), 3) for v in t],
+            "t_max": float(np.abs(t).max()), "rel_diff_frame_mean": [float(v) for v in rel],
+            "nan_single": int(np.isnan(x).any(1).sum()), "nan_sharded": int(np.isnan(y).any(1).sum())}
+
+
+def ttest_consistent(st: dict, t_max: float = 4.5) -> bool:
+    """sample_shard_ttest's verdict: every channel within t_max standard
+    errors (Student-t, >= 64 blocks: |t| > 4.5 has p < 1e-4) and NaN pixel
+    counts within Poisson noise of each other."""
+    a, b = st["nan_single"], st["nan_sharded"]
+    return st["n"] > 0 and st["t_max"] < t_max and abs(a - b) <= 5 * np.sqrt(a + b) + 3
+
+
+def shards_consistent(st: dict) -> bool:
+    """The frame-level bounds of tests/_util.assert_shards_consistent (the
+    per-pixel outlier bound needs G >= 4 shards: with fewer the per-pixel
+    variance estimate has too few degrees of freedom for a 5-sd test)."""
+    if st["n"] <= 0 or abs(st["z_total"]) >= 4 or not 0.5 < st["ratio"] < 2.0 or not 0.3 < st["norm_ratio"] < 3.0:
+        return False
+    a, b = st["nan_single"], st["nan_sharded"]
+    return abs(a - b) <= 5 * np.sqrt(a + b) + 3
 
 
 def _as_like(canvas, a):

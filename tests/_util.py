@@ -70,49 +70,8 @@ def set_scene_from_oracle(device, sc) -> None:
                      arr(sc.tex)[: sc.n_tex], tuple(sc.light_box_pointids[1:5]), sc.light_sphere_point, sc.ior)
 
 
-def sample_shard_consistency(single: np.ndarray, shards: list, spp: int) -> dict:
-    """Monte Carlo consistency of a sample-sharded image with the single-stream
-    image of the same frame (SURVEY.md 8(e) C5 "statistical vs the unsharded
-    reference"; shard.sample_batches).  single: the float32 [n, 4] sums of spp
-    samples per pixel on the reference's stream (seed_base 0); shards: G
-    arrays, each the sums of spp/G samples on its derived stream (seed_base
-    k*n).  The two images are two independent estimates of each pixel's mean
-    radiance, so their per-pixel difference D = (single - sum(shards)) / spp
-    has mean 0 and variance 2 sigma^2 / spp, with sigma^2 the per-sample
-    variance.  sigma^2 / (spp/G) is estimated per pixel from the spread of
-    the G shard means (ddof 1), so Var(D) ~ 2 s^2 / G.  Pixels that are NaN in
-    either image (a non-finite attenuation: the sum stays NaN, MapperPathTracer
-    .cxx:350; NormalizeFunctor zeroes it) are counted, not compared.
-    Returns: n (pixels compared), z_total (sum D / sqrt(sum Var D): ~N(0,1)),
-    ratio (sum D^2 / sum Var D: ~1), outliers (fraction with |D| > 5 sd),
-    norm_ratio (the same ratio after NormalizeFunctor, delta method:
-    Var(sqrt m) ~ Var(m) / (4 m)), nan_single / nan_sharded."""
-    G = len(shards)
-    x = np.asarray(single, np.float64)[:, :3]
-    ys = np.stack([np.asarray(s, np.float64)[:, :3] for s in shards])  # [G, n, 3]
-    nan = np.isnan(x).any(1) | np.isnan(ys).any((0, 2))
-    keep = ~nan
-    x, ys = x[keep], ys[:, keep]
-    mx = x / spp
-    my = ys.sum(0) / spp
-    means = ys / (spp / G)  # per-shard means
-    var_d = 2.0 * means.var(0, ddof=1) / G  # [n, 3]
-    d = mx - my
-    live = var_d > 0
-    z = np.zeros_like(d)
-    z[live] = d[live] / np.sqrt(var_d[live])
-    m = np.maximum(0.5 * (mx + my), 1e-12)
-    nx_, ny_ = np.sqrt(mx), np.sqrt(my)
-    return {
-        "n": int(keep.sum()),
-        "z_total": float(d[live].sum() / np.sqrt(var_d[live].sum())),
-        "ratio": float((d[live] ** 2).sum() / var_d[live].sum()),
-        "outliers": float((np.abs(z) > 5).mean()),
-        "zero_var_nonzero_d": int(((~live) & (d != 0)).sum()),
-        "norm_ratio": float(((nx_ - ny_)[live] ** 2).sum() / (var_d[live] / (4 * m[live])).sum()),
-        "nan_single": int(np.isnan(np.asarray(single)[:, :3]).any(1).sum()),
-        "nan_sharded": int(np.isnan(np.stack([np.asarray(s)[:, :3] for s in shards])).any((0, 2)).sum()),
-    }
+# (the statistic lives in the package: bench.py checks its C5 frames with it)
+from raytracingtherestofyourlife_amd.shard import sample_shard_consistency  # noqa: E402,F401
 
 
 def assert_shards_consistent(st: dict, what: str = "") -> None:

@@ -96,6 +96,10 @@ def test_gpu_lbvh_c3_golden(rtp, device, monkeypatch):
     g = np.load(os.path.join(here, "golden", "c3_subset.npz"), allow_pickle=False)
     monkeypatch.setenv("RTP_BVH_BUILD", "gpu")
     device.set_cornell_box(3)
+    # every direction octant walks its own near-to-far copy on the device-built
+    # tree too (the mask was once cleared to 0 on this branch, so
+    # every ray walked copy 0 -- same bits, slower walks)
+    assert device.sphere_walk_oct_mask() == 7
     pix = g["pixels"][:256]
     got = device.render_pixels(rtp.default_camera(), int(g["nx"]), int(g["ny"]), int(g["spp"]), int(g["depth"]), pix)
     want = (np.concatenate([g["rgb"][:256], np.zeros((256, 1), np.float32)], 1), g["final_seed"][:256], g["live"][:256])
@@ -133,8 +137,10 @@ def test_lds_walk_matches_oracle_900_spheres(rtp, oracle, device, monkeypatch):
     assert_render_equal(_render(device, rtp, nx, ny, 8, 50, pix), want, "LDS walk, 900 spheres")
     set_scene_from_oracle(device, _oracle_scene(oracle, 1200, 21))
     assert device.sphere_walk() == "global"
+    assert device.sphere_walk_oct_mask() == 7
     device.set_cornell_box(0)
     assert device.sphere_walk() == "scan"
+    assert device.sphere_walk_oct_mask() == -1
 
 
 def test_lds_walk_equals_global_walk_c3(rtp, device, monkeypatch):

@@ -174,3 +174,44 @@ def test_overlapped_canvas_reduce(tmp_path, overlap):
     for r in range(world):
         want[r::world] = 100 * 4 + r + 1
     assert np.array_equal(got, want)
+
+
+def _overlap_samples_worker(rank, world, port, overlap, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from raytracingtherestofyourlife_amd import shard
+
+    render = _oracle_render()
+    b = shard.sample_batches(SPP, world, NX * NY)[rank]
+    part = torch.from_numpy(render(None, b.spp, b.seed_base))
+    canvas = torch.zeros((NX * NY, 4), dtype=torch.float32)
+    red = shard.OverlappedCanvasReduce(canvas, dist, overlap=overlap)
+    last = None
+    for step in range(3):  # bench.py's C5 steps: the rank's whole-canvas sample batch, one reduce each
+        last = red.step(None, part)
+    red.drain()
+    if rank == 0:
+        np.save(out_path, last.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_overlapped_reduce_of_sample_batches(tmp_path, overlap):
+    """bench.py's C5 path (--workload c5, N > 1) on CPU: each rank's sample
+    batch of every pixel (seed_base k*N, the oracle standing in for the
+    device) goes through shard.OverlappedCanvasReduce as a whole canvas
+    (ids None) for several steps; rank 0 ends with the shards' sum, NaN
+    pixels carried through."""
+    from raytracingtherestofyourlife_amd import shard
+
+    world = 2
+    out = str(tmp_path / "ovs.npy")
+    mp.start_processes(_overlap_samples_worker, args=(world, _free_port(), overlap, out), nprocs=world, join=True,
+                       start_method="spawn")
+    got = np.load(out)
+    render = _oracle_render()
+    parts = [render(None, b.spp, b.seed_base) for b in shard.sample_batches(SPP, world, NX * NY)]
+    want = parts[0] + parts[1]
+    assert np.isnan(want[:, :3]).any()
+    assert _same(got[:, :3], want[:, :3])
