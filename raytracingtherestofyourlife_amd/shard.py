@@ -243,7 +243,7 @@ def ttest_consistent(st: dict, t_max: float = 4.5) -> bool:
     errors (Student-t, >= 64 blocks: |t| > 4.5 has p < 1e-4) and NaN pixel
     counts within Poisson noise of each other."""
     a, b = st["nan_single"], st["nan_sharded"]
-    return st["n"] > 0 and st["t_max"] < t_max and abs(a - b) <= 5 * np.sqrt(a + b) + 3
+    return bool(st["n"] > 0 and st["t_max"] < t_max and abs(a - b) <= 5 * np.sqrt(a + b) + 3)
 
 
 def shards_consistent(st: dict) -> bool:
@@ -253,7 +253,7 @@ def shards_consistent(st: dict) -> bool:
     if st["n"] <= 0 or abs(st["z_total"]) >= 4 or not 0.5 < st["ratio"] < 2.0 or not 0.3 < st["norm_ratio"] < 3.0:
         return False
     a, b = st["nan_single"], st["nan_sharded"]
-    return abs(a - b) <= 5 * np.sqrt(a + b) + 3
+    return bool(abs(a - b) <= 5 * np.sqrt(a + b) + 3)
 
 
 def _as_like(canvas, a):
