@@ -388,8 +388,11 @@ def main() -> None:
         render()
         return gather_canvas()
 
+    # (the first frame after setup is timed on one GPU only: at N > 1 a C5
+    # frame takes seconds, and the warmup renders it anyway)
     t_first = time.perf_counter()
-    render()
+    if world == 1:
+        render()
     torch.cuda.synchronize()
     t_first_done = time.perf_counter()
     for i in range(args.warmup):  # the first also counts live bounces (for the byte model)
@@ -611,7 +614,7 @@ def main() -> None:
             "bit_exact": None if quality is None else quality["bit_exact"],
             "quality": quality,
             "setup": setup,
-            "first_render_ms": round(first_ms, 2),
+            "first_render_ms": round(first_ms, 2) if world == 1 else None,
             "one_shot": None if world > 1 else {
                 "note": "a fresh process rendering this frame once, like main.cc (its timer, :584-585, 661-663; "
                         "process start, imports and the HIP runtime's first-use initialisation excluded): "

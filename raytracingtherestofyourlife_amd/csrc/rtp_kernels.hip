@@ -57,7 +57,10 @@ constexpr int kHistChunk = 4;
 #ifndef RTP_BVH_DEFER_Q
 #define RTP_BVH_DEFER_Q 2  // queued sphere leaves per lane (1 or 2)
 #endif
-constexpr int kDeferQ = RTP_BVH_DEFER_Q;
+#ifndef RTP_BVH_DEFER_REG
+#define RTP_BVH_DEFER_REG 0  // 1: the queued leaf's 16-byte record kept in registers (queue of one), no re-read
+#endif
+constexpr int kDeferQ = RTP_BVH_DEFER_REG ? 1 : RTP_BVH_DEFER_Q;
 static_assert(kDeferQ == 1 || kDeferQ == 2, "the leaf queue holds one or two node indices");
 #ifndef RTP_CRIT_FF
 #define RTP_CRIT_FF 100  // pool kernel: lag (per mille of the wave's average samples) that makes a pixel critical
@@ -1058,6 +1061,7 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
   // flush pass, which runs when at least RTP_BVH_DEFER lanes hold one
   constexpr bool kDefer = kWalk && !kLdsBvh && RTP_BVH_DEFER > 0;
   int wqn = 0, wq0 = 0, wq1 = 0;            // the path's queued sphere leaves (node indices)
+  u4v wqv = u4v{0u, 0u, 0u, 0u};            // RTP_BVH_DEFER_REG: the queued leaf's record (one entry)
   Path ps;
   ps.org = eye;
   ps.dir = mk(0.f, 0.f, 1.f);
@@ -1323,7 +1327,7 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
               const int ni = wq0;
               wq0 = wq1;
               wqn--;
-              const u4v sv = node(ni);
+              const u4v sv = RTP_BVH_DEFER_REG ? wqv : node(ni);
               float t;
               if (sphere_root(o, d, 0.001f, mk(__uint_as_float(sv.x), __uint_as_float(sv.y), __uint_as_float(sv.z)),
                               __uint_as_float(sv.w & ~kCBvhSphereBit), t))
@@ -1341,6 +1345,7 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
                 if (!blocked) {
                   if (wqn == 0) wq0 = wni;
                   else wq1 = wni;
+                  if (RTP_BVH_DEFER_REG) wqv = v;
                   wqn++;
                 }
                 next = blocked ? wni : wni + 1;
