@@ -49,19 +49,6 @@ constexpr int kHistChunk = 4;
 // many of the wave's paths have finished their walks (or all have)
 #define RTP_WALK_DONE 48
 #endif
-#ifndef RTP_BVH_DEFER
-// pool kernel, global sphere-BVH walk: flush the queued sphere leaves when at
-// least this many lanes hold one (0: every sphere leaf tested when visited)
-#define RTP_BVH_DEFER 0
-#endif
-#ifndef RTP_BVH_DEFER_Q
-#define RTP_BVH_DEFER_Q 2  // queued sphere leaves per lane (1 or 2)
-#endif
-#ifndef RTP_BVH_DEFER_REG
-#define RTP_BVH_DEFER_REG 0  // 1: the queued leaf's 16-byte record kept in registers (queue of one), no re-read
-#endif
-constexpr int kDeferQ = RTP_BVH_DEFER_REG ? 1 : RTP_BVH_DEFER_Q;
-static_assert(kDeferQ == 1 || kDeferQ == 2, "the leaf queue holds one or two node indices");
 #ifndef RTP_CRIT_FF
 #define RTP_CRIT_FF 100  // pool kernel: lag (per mille of the wave's average samples) that makes a pixel critical
 #endif
@@ -1057,11 +1044,6 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
   constexpr bool kWalk = kBvh;
   int wni = -1;                             // the path's next BVH node; -1: its quads are not scanned yet
   Hit wh{3.40282347e+38f, -1, 0};           // its closest hit so far
-  // RTP_BVH_DEFER > 0 (the global walk): sphere leaves queued for a later
-  // flush pass, which runs when at least RTP_BVH_DEFER lanes hold one
-  constexpr bool kDefer = kWalk && !kLdsBvh && RTP_BVH_DEFER > 0;
-  int wqn = 0, wq0 = 0, wq1 = 0;            // the path's queued sphere leaves (node indices)
-  u4v wqv = u4v{0u, 0u, 0u, 0u};            // RTP_BVH_DEFER_REG: the queued leaf's record (one entry)
   Path ps;
   ps.org = eye;
   ps.dir = mk(0.f, 0.f, 1.f);
@@ -1293,7 +1275,7 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
       const uint64_t pm = __ballot(has_path);
       const int need = min(RTP_WALK_DONE, __popcll(pm));
       bool walking = has_path && wni < nn;
-      if (__ballot(walking || (kDefer && wqn > 0))) {
+      if (__ballot(walking)) {
         const f3 o = ps.org, d = ps.dir;
         const BvhRay R = bvh_ray<kLdsBvh>(sc, o, d);
         GF4* __restrict__ geom_g = (GF4*)sc->sph_geom;
@@ -1310,73 +1292,19 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
         };
         u4v v = u4v{0u, 0u, 0u, 0u};
         if (walking) v = node(wni);
-        if constexpr (kDefer) {
-          // Deferred sphere leaves (RTP_BVH_DEFER): a walk iteration only
-          // tests boxes; a sphere leaf's node index goes to the lane's queue
-          // (up to kDeferQ entries, the walk moves on to the next node) and a
-          // flush pass -- one queued sphere per lane, the node re-read --
-          // runs the exact root test when enough lanes hold one, when a lane
-          // is blocked on a full queue, or when lanes that finished their
-          // walk wait on their queue.  Without it every iteration ran the
-          // sphere test for the ~11% of lanes at a leaf (C3: ~55 VALU beside
-          // a ~15-VALU box test).  The boxes cull against the hit found so
-          // far, which may now lag: a walk can only visit MORE nodes, and the
-          // (t, index) minimum over the tested spheres is the same.
-          auto flush = [&] {
-            if (wqn > 0) {
-              const int ni = wq0;
-              wq0 = wq1;
-              wqn--;
-              const u4v sv = RTP_BVH_DEFER_REG ? wqv : node(ni);
-              float t;
-              if (sphere_root(o, d, 0.001f, mk(__uint_as_float(sv.x), __uint_as_float(sv.y), __uint_as_float(sv.z)),
-                              __uint_as_float(sv.w & ~kCBvhSphereBit), t))
-                bvh_accept(wh, t, 2, ni, R, [&] { return R.cidx[ni]; });
-            }
-          };
-          for (;;) {
-            const uint64_t wm = __ballot(walking), qm = __ballot(wqn > 0);
-            if ((wm | qm) == 0 || __popcll(pm & ~wm & ~qm) >= need) break;
-            bool blocked = false;
-            if (walking) {
-              int next;
-              if ((int32_t)v.w < 0) {  // a sphere leaf: queued (or, queue full, retried after the flush)
-                blocked = wqn >= kDeferQ;
-                if (!blocked) {
-                  if (wqn == 0) wq0 = wni;
-                  else wq1 = wni;
-                  if (RTP_BVH_DEFER_REG) wqv = v;
-                  wqn++;
-                }
-                next = blocked ? wni : wni + 1;
-              } else {
-                next = bvh_visit<false>(geom_g, lsph, R, o, d, v, wni, wh);
-              }
-              walking = next < nn;
-              if (walking && next != wni) v = node(next);
-              wni = next;
-            }
-            const uint64_t wm2 = __ballot(walking), qm2 = __ballot(wqn > 0);
-            if (__ballot(blocked) || wm2 == 0 || __popcll(qm2) >= RTP_BVH_DEFER ||
-                __popcll(pm & ~wm2) >= need)
-              flush();
+        for (;;) {
+          const uint64_t wm = __ballot(walking);
+          if (wm == 0 || __popcll(pm & ~wm) >= need) break;
+          if (walking) {
+            const int next = bvh_visit<kLdsBvh>(geom_g, lsph, R, o, d, v, wni, wh);
+            walking = next < nn;
+            if (walking) v = node(next);
+            wni = next;
           }
-          if (has_path && !walking && wqn == 0) bvh_resolve(wh, R);
-        } else {
-          for (;;) {
-            const uint64_t wm = __ballot(walking);
-            if (wm == 0 || __popcll(pm & ~wm) >= need) break;
-            if (walking) {
-              const int next = bvh_visit<kLdsBvh>(geom_g, lsph, R, o, d, v, wni, wh);
-              walking = next < nn;
-              if (walking) v = node(next);
-              wni = next;
-            }
-          }
-          if (has_path && !walking) bvh_resolve(wh, R);
         }
+        if (has_path && !walking) bvh_resolve(wh, R);
       }
-      shade = has_path && !walking && !(kDefer && wqn > 0);
+      shade = has_path && !walking;
       if (want_dbg) dbg[kDbgCyclesIntersect] += stamp(want_dbg) - ta;
     }
     if (shade) {
