@@ -35,3 +35,26 @@ def test_bench_rccl_reduce_path_on_one_rank():
     assert line["check_reduced_canvas_equals_single_render"] is True
     log = r.stdout + r.stderr
     assert "NCCL INFO" in log, log[-2000:]
+
+
+def test_bench_rccl_sample_shard_path_on_one_rank():
+    """bench.py's C5 path (--workload c5) through RCCL on one rank: the
+    all_gather of the shard-check codes and of the shards' check pixels, the
+    whole-canvas copy into the overlapped reduce, rank 0's same-workload
+    one-GPU render and the reduced-canvas checks (one rank: the reduce is the
+    identity, so the reduced canvas equals the shard exactly)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", "29657", "bench.py", "--gpus", "1",
+           "--force-collective", "--dist-backend", "nccl", "--workload", "c5", "--nx", "96", "--ny", "64",
+           "--spp", "64", "--depth", "20", "--steps", "2", "--warmup", "1", "--ff-tables", "off", "--check"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert line["config"]["dist_backend"] == "nccl" and "sample batches" in line["config"]["shard"]
+    chk = line["check_reduced_canvas"]
+    assert chk["reduced_equals_sum_of_shards_max_rel"] == 0.0 and chk["nan_pattern_equal"]
+    assert chk["consistent"] is True
+    assert line["speedup_vs_one_gpu_same_workload"] > 0
