@@ -334,47 +334,6 @@ RTP_DEV f2v dot_m2l(const float* x, const f2v (&y)[3]) {  // dot_m with a shared
   else return f2v{0.0f, 0.0f};
 }
 
-// The exact-parallelogram path of quad_hit_masked<K> (e21 == -e03 and
-// e23 == -e01 bit for bit): Pp == -P, detp == det, Qp == -cross(Tp, e01), so
-// the second triangle is the first one's arithmetic on Tp = o - v11 with both
-// results negated (negation commutes with rounding).  Half .x is the (v00)
-// triangle, .y the (v11) one; both always evaluated, branch-free.  G: a
-// QuadGeom-layout head (SGPRs in the scan; VGPRs for the prefilter's
-// candidates, whose heads come from the block's LDS table).  With K = 0 (every
-// edge component kept) the products with exactly-zero components of a
-// structured quad are +-0 and leave every other value unchanged,
-// so the generic form returns the kind's own bits.
-template <int K, class G>
-RTP_DEV bool quad_hit_para(const G& Q, f3 o, f3 d, float& t_out) {
-  constexpr int M01 = kQuadKind[K].m01, M03 = kQuadKind[K].m03;
-  constexpr int MP = cross_mask(M03), MQ = cross_mask(M01);
-  const float dv[3] = {d.x, d.y, d.z};
-  const float P[3] = {cross_c<M03, 0>(dv, Q.e03), cross_c<M03, 1>(dv, Q.e03), cross_c<M03, 2>(dv, Q.e03)};
-  const float det = dot_m<M01 & MP>(Q.e01, P);
-  const float inv_det = rcp_det(det);
-  const float ov[3] = {o.x, o.y, o.z};
-  const f2v T2[3] = {f2v{ov[0], ov[0]} - f2v{Q.vv[0][0], Q.vv[0][1]},
-                     f2v{ov[1], ov[1]} - f2v{Q.vv[1][0], Q.vv[1][1]},
-                     f2v{ov[2], ov[2]} - f2v{Q.vv[2][0], Q.vv[2][1]}};
-  const f2v al2 = dot_m2<MP>(T2, P) * inv_det;  // (alpha, -ap)
-  const f2v Q2[3] = {cross_c2<M01, 0>(T2, Q.e01), cross_c2<M01, 1>(T2, Q.e01), cross_c2<M01, 2>(T2, Q.e01)};
-  const f2v be2 = dot_m2l<MQ>(dv, Q2) * inv_det;  // (beta, -bp)
-  const float Qv[3] = {Q2[0].x, Q2[1].x, Q2[2].x};
-  const float t = dot_m<M03 & MQ>(Q.e03, Qv) * inv_det;
-  const float alpha = al2.x, beta = be2.x;
-  // ap < 0 <=> -al2.y < 0 <=> al2.y > 0 (NaN: false both ways; -(+-0) is
-  // not < 0 and +-0 is not > 0), likewise bp; evaluated without short
-  // circuits so no lane mask or max canonicalisation is generated;
-  // !(a < 0) & !(b < 0) & !(c < 0) == !(minNum(a, b, c) < 0): minNum skips
-  // NaN operands, whose terms are true (!(NaN < 0)); all three NaN gives
-  // NaN, true as well; -0 is not < 0 either way (no signaling NaNs arise)
-  const bool ok1 = !(fabsf(det) < kEps) & !(fminf(fminf(alpha, beta), t) < 0.0f);
-  const bool second = (alpha + beta) > 1.0f;
-  const bool bad2 = (al2.y > 0.0f) | (be2.y > 0.0f);
-  t_out = t;
-  return ok1 & !(second & bad2);
-}
-
 // G: the quad's scan head (a DevQuad, or a QuadGeom copy already in
 // registers); M: the quad in memory, read only for the second triangle's
 // edges of a quad that is not an exact parallelogram.
@@ -382,13 +341,40 @@ template <int K, class G = DevQuad>
 RTP_DEV bool quad_hit_masked(const G& Q, const DevQuad& M, f3 o, f3 d, float& t_out) {
   constexpr int M01 = kQuadKind[K].m01, M03 = kQuadKind[K].m03, M21 = kQuadKind[K].m21, M23 = kQuadKind[K].m23;
   constexpr int MP = cross_mask(M03), MQ = cross_mask(M01), MPp = cross_mask(M21), MQp = cross_mask(M23);
-  // (a parallelogram has e21 == -e03 and e23 == -e01, so only kinds whose
-  // masks pair up can hold one)
-  if constexpr (M21 == M03 && M23 == M01) if (Q.para) return quad_hit_para<K>(Q, o, d, t_out);
   const float dv[3] = {d.x, d.y, d.z};
   const float P[3] = {cross_c<M03, 0>(dv, Q.e03), cross_c<M03, 1>(dv, Q.e03), cross_c<M03, 2>(dv, Q.e03)};
   const float det = dot_m<M01 & MP>(Q.e01, P);
   const float inv_det = rcp_det(det);
+  // (a parallelogram has e21 == -e03 and e23 == -e01, so only kinds whose
+  // masks pair up can hold one)
+  if constexpr (M21 == M03 && M23 == M01) if (Q.para) {
+    // exact parallelogram (e21 == -e03, e23 == -e01 bit for bit): Pp == -P,
+    // detp == det, Qp == -cross(Tp, e01), so the second triangle is the first
+    // one's arithmetic on Tp = o - v11 with both results negated (negation
+    // commutes with rounding).  Half .x is the (v00) triangle, .y the (v11)
+    // one; both always evaluated, branch-free.
+    const float ov[3] = {o.x, o.y, o.z};
+    const f2v T2[3] = {f2v{ov[0], ov[0]} - f2v{Q.vv[0][0], Q.vv[0][1]},
+                       f2v{ov[1], ov[1]} - f2v{Q.vv[1][0], Q.vv[1][1]},
+                       f2v{ov[2], ov[2]} - f2v{Q.vv[2][0], Q.vv[2][1]}};
+    const f2v al2 = dot_m2<MP>(T2, P) * inv_det;  // (alpha, -ap)
+    const f2v Q2[3] = {cross_c2<M01, 0>(T2, Q.e01), cross_c2<M01, 1>(T2, Q.e01), cross_c2<M01, 2>(T2, Q.e01)};
+    const f2v be2 = dot_m2l<MQ>(dv, Q2) * inv_det;  // (beta, -bp)
+    const float Qv[3] = {Q2[0].x, Q2[1].x, Q2[2].x};
+    const float t = dot_m<M03 & MQ>(Q.e03, Qv) * inv_det;
+    const float alpha = al2.x, beta = be2.x;
+    // ap < 0 <=> -al2.y < 0 <=> al2.y > 0 (NaN: false both ways; -(+-0) is
+    // not < 0 and +-0 is not > 0), likewise bp; evaluated without short
+    // circuits so no lane mask or max canonicalisation is generated;
+    // !(a < 0) & !(b < 0) & !(c < 0) == !(minNum(a, b, c) < 0): minNum skips
+    // NaN operands, whose terms are true (!(NaN < 0)); all three NaN gives
+    // NaN, true as well; -0 is not < 0 either way (no signaling NaNs arise)
+    const bool ok1 = !(fabsf(det) < kEps) & !(fminf(fminf(alpha, beta), t) < 0.0f);
+    const bool second = (alpha + beta) > 1.0f;
+    const bool bad2 = (al2.y > 0.0f) | (be2.y > 0.0f);
+    t_out = t;
+    return ok1 & !(second & bad2);
+  }
   const float T[3] = {o.x - Q.vv[0][0], o.y - Q.vv[1][0], o.z - Q.vv[2][0]};
   const float alpha = dot_m<MP>(T, P) * inv_det;
   const float Qv[3] = {cross_c<M01, 0>(T, Q.e01), cross_c<M01, 1>(T, Q.e01), cross_c<M01, 2>(T, Q.e01)};

@@ -131,18 +131,11 @@ bool bit_equal(const float* a, const float* b, int n) { return std::memcmp(a, b,
 // vertices in the other two coordinates, widened outward by a few ulps so
 // that the float box contains the real one.  Enabled only when every such
 // quad qualifies, they fit kMaxPre, and the scene is within the coordinate
-// range the kernel's error margins assume (|x| <= kPreLim).  Then, when every
-// quad of groups 6 and 7 (kinds 7 and 8) is the vertical face of a box
-// rotated about y -- an exact parallelogram whose vertices share x and z
-// pairwise and y pairwise, bit for bit -- those join it as PreVert records:
-// the face's plane nx x + nz z = c (unit normal in double, rounded) and its
-// extent along e = (nz, -nx) and y, widened.  Every prefiltered quad's scan
-// head goes to prex[] (the candidates' exact test).  RTP_PREFILTER=0 turns
-// the prefilter off, RTP_PREFILTER_VERT=0 keeps kinds 7, 8 in the exact scan.
+// range the kernel's error margins assume (|x| <= kPreLim).
 constexpr float kPreLim = 16.0f;
 void setup_prefilter(rtp::DevScene* h, const rtp_scene_desc* s, const std::vector<int>& kept) {
   h->n_pre = 0;
-  for (int a = 0; a <= 4; a++) h->pre_begin[a] = 0;
+  for (int a = 0; a <= 3; a++) h->pre_begin[a] = 0;
   h->pre_scale = 0.0f;
   const int n = h->kind_begin[6];
   if (n <= 0 || n > rtp::kMaxPre) return;
@@ -151,9 +144,6 @@ void setup_prefilter(rtp::DevScene* h, const rtp_scene_desc* s, const std::vecto
   std::vector<int> axis_of(n);
   std::vector<rtp::PreQuad> pq(n);
   float scale = 0.0f;
-  auto head_of = [&](int q) {  // the candidate's exact-test record: the quad's 64-byte scan head
-    std::memcpy(&h->prex[q], &h->quads[q], sizeof(rtp::QuadGeom));
-  };
   for (int q = 0; q < n; q++) {
     const rtp::DevQuad& Q = h->quads[q];
     const rtp::QuadKindMasks& K = rtp::kQuadKind[Q.kind];
@@ -161,7 +151,19 @@ void setup_prefilter(rtp::DevScene* h, const rtp_scene_desc* s, const std::vecto
     if (Q.kind < 1 || Q.kind > 6 || (flat != 1 && flat != 2 && flat != 4)) return;
     const int a = flat == 1 ? 0 : flat == 2 ? 1 : 2, b = (a + 1) % 3, c = (a + 2) % 3;
     if (!Q.para) return;  // (unreachable: kinds 1..6 are exact parallelograms, see fill_quad)
-    head_of(q);
+    {
+      const int ei = K.m01 == 1 ? 0 : K.m01 == 2 ? 1 : 2, ej = K.m03 == 1 ? 0 : K.m03 == 2 ? 1 : 2;
+      const int ea = 3 - ei - ej;
+      rtp::PreExact& E = h->prex[q];
+      std::memset(&E, 0, sizeof(E));
+      E.i = ei;
+      E.s = (ej == (ei + 1) % 3) ? 1 : -1;
+      E.b = Q.e01[ei], E.c = Q.e03[ej];
+      E.bs = E.s > 0 ? E.b : -E.b, E.cs = E.s > 0 ? E.c : -E.c;
+      E.vi = Q.vv[ei][0], E.va = Q.vv[ea][0], E.vj = Q.vv[ej][0];
+      E.wi = Q.vv[ei][1], E.wa = Q.vv[ea][1], E.wj = Q.vv[ej][1];
+      E.key_lo = Q.key_lo;
+    }
     const int32_t* id = s->quad_points + 4 * kept[Q.orig];
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     const float x = s->points[3 * id[0] + a];
@@ -196,61 +198,9 @@ void setup_prefilter(rtp::DevScene* h, const rtp_scene_desc* s, const std::vecto
     for (int q = 0; q < n; q++)
       if (axis_of[q] == a) h->pre[pos++] = pq[q];
   }
-  h->pre_begin[3] = h->pre_begin[4] = pos;
+  h->pre_begin[3] = pos;
   h->pre_scale = scale;
   h->n_pre = n;
-  // the vertical faces of boxes rotated about y (groups 6, 7)
-  const int nv_end = h->kind_begin[8];
-  const char* ev = getenv("RTP_PREFILTER_VERT");
-  if ((ev && ev[0] == '0') || nv_end == n || nv_end > rtp::kMaxPre) return;
-  std::vector<rtp::PreVert> pv;
-  float vscale = scale;
-  for (int q = n; q < nv_end; q++) {
-    const rtp::DevQuad& Q = h->quads[q];
-    if (!Q.para || (Q.kind != 7 && Q.kind != 8)) return;
-    const int32_t* id = s->quad_points + 4 * kept[Q.orig];
-    const float* v00 = s->points + 3 * id[0];
-    const float* v10 = s->points + 3 * id[1];
-    const float* v11 = s->points + 3 * id[2];
-    const float* v01 = s->points + 3 * id[3];
-    // kind 7: e01 = v10 - v00 horizontal, e03 = v01 - v00 vertical; kind 8: the other way round
-    const float* hA = v00;
-    const float* hB = Q.kind == 7 ? v10 : v01;  // the horizontal edge's far end
-    const float* vB = Q.kind == 7 ? v01 : v10;  // the vertical edge's far end
-    auto same_xz = [](const float* p, const float* q2) { return p[0] == q2[0] && p[2] == q2[2]; };
-    if (!same_xz(hA, vB) || !same_xz(hB, v11) || !(hA[1] == hB[1]) || !(vB[1] == v11[1])) return;
-    for (const float* p : {v00, v10, v11, v01})
-      for (int j = 0; j < 3; j++) {
-        if (!std::isfinite(p[j])) return;
-        vscale = std::max(vscale, std::fabs(p[j]));
-      }
-    const double dx = (double)hB[0] - hA[0], dz = (double)hB[2] - hA[2], L = std::hypot(dx, dz);
-    if (!(L > 0.0)) return;
-    const double nx = -dz / L, nz = dx / L;  // unit normal in xz; e = (nz, -nx) = (dx, dz) / L
-    rtp::PreVert V;
-    std::memset(&V, 0, sizeof(V));
-    V.nx = (float)nx;
-    V.nz = (float)nz;
-    V.c = (float)(nx * hA[0] + nz * hA[2]);
-    const double ua = nz * hA[0] - nx * hA[2], ub = nz * hB[0] - nx * hB[2];
-    const double ya = hA[1], yb = vB[1];
-    auto centre_half = [](double lo, double hi, float& cen, float& half) {
-      if (lo > hi) std::swap(lo, hi);
-      cen = (float)(0.5 * (lo + hi));
-      half = (float)std::max(hi - (double)cen, (double)cen - lo);
-      for (int u = 0; u < 2; u++) half = std::nextafter(half, INFINITY);
-    };
-    centre_half(ua, ub, V.cu, V.ru);
-    centre_half(ya, yb, V.cy, V.ry);
-    V.qpos = q;
-    pv.push_back(V);
-  }
-  if (!(vscale <= kPreLim) || pos + (int)pv.size() > rtp::kMaxPre) return;
-  for (const rtp::PreVert& V : pv) std::memcpy(&h->pre[pos++], &V, sizeof(V));
-  for (int q = n; q < nv_end; q++) head_of(q);
-  h->pre_begin[4] = pos;
-  h->pre_scale = vscale;
-  h->n_pre = nv_end;
 }
 
 // RNG jump tables.  A dead depth consumes 1 + {2,3,2} draws chosen by the

@@ -342,15 +342,9 @@ typedef uint32_t u8v __attribute__((ext_vector_type(8)));
 RTP_DEV u8v pre_rec(const DevScene* __restrict__ sc, int i) {
   return reinterpret_cast<const u8v*>(sc->pre)[min(i, kMaxPre - 1)];
 }
-// k1 <= k2 <= k3: the three smallest keys (one v_med3 each for k2 and k3)
-RTP_DEV void fold3(uint32_t key, uint32_t& k1, uint32_t& k2, uint32_t& k3) {
-  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(k3) : "v"(k2), "v"(k3), "v"(key));
-  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(k2) : "v"(k1), "v"(k2), "v"(key));
-  k1 = min(k1, key);
-}
 template <int A>
 RTP_DEV void pre_axis(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d, float ma, float mb, uint32_t& k1,
-                      uint32_t& k2, uint32_t& k3, u8v& cur) {
+                      uint32_t& k2, u8v& cur) {
   constexpr int B = (A + 1) % 3, C = (A + 2) % 3;
   if (b == e) return;
   const float inv = __builtin_amdgcn_rcpf(comp<A>(d));
@@ -370,7 +364,10 @@ RTP_DEV void pre_axis(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d,
     asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(key) : "v"(__float_as_uint(t - m)), "v"(~31u), "s"((uint32_t)P.qpos));
     return ok ? key : ~0u;
   };
-  auto fold = [&](uint32_t key) { fold3(key, k1, k2, k3); };
+  auto fold = [&](uint32_t key) {  // keep the two smallest keys
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(k2) : "v"(k1), "v"(k2), "v"(key));
+    k1 = min(k1, key);
+  };
   // ping-pong heads, pointer walk (as scan_kind_pf; prefetches past pre[]
   // stay inside DevScene: prex[] follows)
   auto as_pre = [](const u8v& v) {
@@ -391,70 +388,39 @@ RTP_DEV void pre_axis(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d,
   }
 }
 
-// The vertical faces of boxes rotated about y (PreVert, kinds 7 and 8): the
-// same candidate keys in the face's own frame.  t = (c - n.o) / (n.d) and the
-// hit point's offsets along e = (nz, -nx) and y from the face's centre, each
-// from a few roundings of unit-normal products; the Lagae-Dutre test's own t
-// has a cancellation in det = e01.(d x e03) ~ |e01| h (n.d), so both errors
-// grow like 1 / |n.d| (the grazing factor).  Margins (both computations' error
-// bounds, ~2^-19 (|o| + scale + 2 |t| |d|) / |n.d|, times 16):
-//   m  = (2^-14 max(|d|max, 1) |t| + 2^-15 (|o|max + scale + 1)) / |n.d|  on t,
-//   mi = m (max(|d|max, 1) + 1)                                         in the plane;
-// a face the exact test accepts (t > 0.001) has t_a + m > 0.001, its hit
-// point within mi of the face's (widened) rectangle, and key t_a - m
-// (clamped at 0) <= its exact t.  n.d = 0 (or NaN) makes no candidate: the
-// exact test rejects such a face (|det| < 1e-5).
-RTP_DEV void pre_vert(const DevScene* __restrict__ sc, int b, int e, f3 o, f3 d, float ma, float mb, float mia,
-                      float mib, uint32_t& k1, uint32_t& k2, uint32_t& k3, u8v& cur) {
-  if (b == e) return;
-  auto key_of = [&](const PreVert& V) -> uint32_t {
-    const float no = __builtin_fmaf(V.nx, o.x, V.nz * o.z), nd = __builtin_fmaf(V.nx, d.x, V.nz * d.z);
-    const float inv = __builtin_amdgcn_rcpf(nd);
-    const float t = (V.c - no) * inv;
-    const float eo = __builtin_fmaf(V.nz, o.x, -(V.nx * o.z)), ed = __builtin_fmaf(V.nz, d.x, -(V.nx * d.z));
-    const float pu = __builtin_fmaf(t, ed, eo) - V.cu, py = __builtin_fmaf(t, d.y, o.y) - V.cy;
-    const float ai = fabsf(inv), at = fabsf(t);
-    const float m = __builtin_fmaf(at, ma, mb) * ai, mi = __builtin_fmaf(at, mia, mib) * ai;
-    const bool ok = (fmaxf(fabsf(pu) - V.ru, fabsf(py) - V.ry) <= mi) & (t + m > 0.001f);
-    uint32_t key;
-    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(key) : "v"(__float_as_uint(fmaxf(t - m, 0.0f))), "v"(~31u),
-        "s"((uint32_t)V.qpos));
-    return ok ? key : ~0u;
+// quad_hit_masked<K>'s parallelogram path for an axis-plane quad of any of
+// the kinds 1..6, the kind chosen per lane: the same products, sums and
+// signs (derived in DESIGN.md 4.1), on o and d permuted into the quad's axes.
+RTP_DEV bool quad_hit_axis(const PreExact& E, f3 o, f3 d, float& t_out) {
+  const bool x0 = E.i == 0, x1 = E.i == 1, pos = E.s > 0;
+  auto perm = [&](f3 v, float& vi, float& va, float& vj) {
+    const float r0 = x0 ? v.x : (x1 ? v.y : v.z);
+    const float r1 = x0 ? v.y : (x1 ? v.z : v.x);
+    const float r2 = x0 ? v.z : (x1 ? v.x : v.y);
+    vi = r0;
+    vj = pos ? r1 : r2;
+    va = pos ? r2 : r1;
   };
-  auto as_vert = [](const u8v& v) {
-    PreVert V;
-    __builtin_memcpy(&V, &v, sizeof(V));
-    return V;
-  };
-  // ping-pong records as pre_axis (prefetches past pre[] stay inside DevScene)
-  const PreQuad* pq = sc->pre + b;
-  for (int n = e - b; n > 0; n -= 2, pq += 2) {
-    const u8v nxt = *reinterpret_cast<const u8v*>(pq + 1);
-    fold3(key_of(as_vert(cur)), k1, k2, k3);
-    if (n == 1) {
-      cur = nxt;
-      break;
-    }
-    cur = *reinterpret_cast<const u8v*>(pq + 2);
-    fold3(key_of(as_vert(nxt)), k1, k2, k3);
-  }
-}
-
-// The exact test of a prefilter candidate: the generic parallelogram test
-// (quad_hit_para<0>, bit-identical to every kind's own) on the
-// candidate's scan head, four 16-byte reads from the block's LDS table (every
-// lane reads: a lane without a candidate reads record 31, in bounds, unused).
-// Returns the (t, orig) key of an accepted hit (t > 0.001), else kNoHitKey.
-RTP_DEV uint64_t pre_exact(const float* lds_prex, uint32_t k, f3 o, f3 d) {
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  const f4v* lx = reinterpret_cast<const f4v*>(lds_prex) + 4 * (k & 31u);
-  f4v xr[4] = {lx[0], lx[1], lx[2], lx[3]};
-  static_assert(sizeof(QuadGeom) == sizeof(xr), "a scan head is four 16-byte loads");
-  QuadGeom Q;
-  __builtin_memcpy(&Q, xr, sizeof(Q));
-  float t;
-  const bool ok = quad_hit_para<0>(Q, o, d, t);
-  return (ok && t > 0.001f) ? ((uint64_t)__float_as_uint(t) << 32 | Q.key_lo) : kNoHitKey;
+  float oi, oa, oj, di, da, dj;
+  perm(o, oi, oa, oj);
+  perm(d, di, da, dj);
+  const float Pa = di * E.cs;     // s * d_i c
+  const float Pi = -(da * E.cs);  // -s * d_a c
+  const float det = E.b * Pi;
+  const float inv_det = rcp_det(det);
+  const f2v Ta = f2v{oa, oa} - f2v{E.va, E.wa};
+  const f2v Ti = f2v{oi, oi} - f2v{E.vi, E.wi};
+  const f2v Tj = f2v{oj, oj} - f2v{E.vj, E.wj};
+  const f2v al2 = (Ti * Pi + Ta * Pa) * inv_det;  // (alpha, -ap)
+  const f2v Qj = Ta * E.bs;                       // s * T_a b
+  const f2v Qa = -(Tj * E.bs);                    // -s * T_j b
+  const f2v be2 = (f2v{dj, dj} * Qj + f2v{da, da} * Qa) * inv_det;  // (beta, -bp)
+  const float t = (E.c * Qj.x) * inv_det;
+  const bool ok1 = !(fabsf(det) < kEps) & !(fminf(fminf(al2.x, be2.x), t) < 0.0f);  // (see quad_hit_masked)
+  const bool second = (al2.x + be2.x) > 1.0f;
+  const bool bad2 = (al2.y > 0.0f) | (be2.y > 0.0f);
+  t_out = t;
+  return ok1 & !(second & bad2);
 }
 
 // kSpheres = false: the quads only (the pool kernel's resumable sphere-BVH
@@ -466,17 +432,14 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
   const float tmin = 0.001f;
   // the (t, orig) key minimum: the order the kinds are scanned in is free
   uint64_t key = kNoHitKey;
-  bool full = true;  // this lane needs the exact scan of the prefiltered quads
-  const bool pre = prefilter && sc->n_pre > 0;                  // wave-uniform
-  const bool vert = pre && sc->pre_begin[4] > sc->pre_begin[3];  // kinds 7, 8 prefiltered too
-  const int g6 = sc->kind_begin[6], g7 = sc->kind_begin[7], g8 = sc->kind_begin[8], g9 = sc->kind_begin[9],
-            g10 = sc->kind_begin[10], g11 = sc->kind_begin[11];
-  {  // kinds 7..10 and 0: the exact scan, always (their keys are final); 7 and 8
-     // left out when the prefilter covers them (empty groups: the head of g8 rides through)
-    const int b7 = vert ? g8 : g6, e7 = vert ? g8 : g7, e8 = g8;
-    u16v cur = quad_head(sc, b7);
-    scan_kind_pf<7>(sc, b7, e7, o, d, key, cur);
-    scan_kind_pf<8>(sc, e7, e8, o, d, key, cur);
+  bool full = true;  // this lane needs the exact scan of the axis-plane quads (kinds 1..6)
+  const bool pre = prefilter && sc->n_pre > 0;  // wave-uniform
+  {  // kinds 7..10 and 0: the exact scan, always (their keys are final)
+    const int g6 = sc->kind_begin[6], g7 = sc->kind_begin[7], g8 = sc->kind_begin[8], g9 = sc->kind_begin[9],
+              g10 = sc->kind_begin[10], g11 = sc->kind_begin[11];
+    u16v cur = quad_head(sc, g6);
+    scan_kind_pf<7>(sc, g6, g7, o, d, key, cur);
+    scan_kind_pf<8>(sc, g7, g8, o, d, key, cur);
     scan_kind_pf<9>(sc, g8, g9, o, d, key, cur);
     scan_kind_pf<10>(sc, g9, g10, o, d, key, cur);
     scan_kind_pf<0>(sc, g10, g11, o, d, key, cur);
@@ -488,43 +451,34 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
     const float dmax = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fmaxf(fabsf(d.z), 1.0f));
     const float omax = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
     const float ma = kPreK * dmax, mb = kPreK * (omax + (sc->pre_scale + 1.0f));
-    uint32_t k1 = ~0u, k2 = ~0u, k3 = ~0u;
+    uint32_t k1 = ~0u, k2 = ~0u;
     const int p0 = sc->pre_begin[0], p1 = sc->pre_begin[1], p2 = sc->pre_begin[2], p3 = sc->pre_begin[3];
     u8v pcur = pre_rec(sc, p0);
-    pre_axis<0>(sc, p0, p1, o, d, ma, mb, k1, k2, k3, pcur);
-    pre_axis<1>(sc, p1, p2, o, d, ma, mb, k1, k2, k3, pcur);
-    pre_axis<2>(sc, p2, p3, o, d, ma, mb, k1, k2, k3, pcur);
-    if (vert) {  // (pcur holds pre[p3], the first vertical face's record)
-      const float va = 0x1p-14f * dmax, vb = 0x1p-15f * (omax + (sc->pre_scale + 1.0f)), vi = dmax + 1.0f;
-      pre_vert(sc, p3, sc->pre_begin[4], o, d, va, vb, va * vi, vb * vi, k1, k2, k3, pcur);
+    pre_axis<0>(sc, p0, p1, o, d, ma, mb, k1, k2, pcur);
+    pre_axis<1>(sc, p1, p2, o, d, ma, mb, k1, k2, pcur);
+    pre_axis<2>(sc, p2, p3, o, d, ma, mb, k1, k2, pcur);
+    // the candidate's PreExact record from the block's LDS table: four
+    // 16-byte reads issued together (every lane: k1 = ~0u reads record 31,
+    // in bounds, unused)
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v* lx = reinterpret_cast<const f4v*>(lds_prex) + 4 * (k1 & 31u);
+    f4v xr[4] = {lx[0], lx[1], lx[2], lx[3]};
+    static_assert(sizeof(PreExact) == sizeof(xr), "PreExact is four 16-byte loads");
+    if (lane_ok && k1 != ~0u) {  // (finite o, d: the generic arithmetic equals the kind's)
+      PreExact Q;
+      __builtin_memcpy(&Q, xr, sizeof(Q));
+      float t;
+      const bool ok = quad_hit_axis(Q, o, d, t);
+      const uint64_t kq = (uint64_t)__float_as_uint(t) << 32 | Q.key_lo;
+      key = (ok && t > 0.001f && kq < key) ? kq : key;
     }
-    // the candidates in key order, each tested exactly while its lower bound
-    // does not exceed the best hit so far (a wave runs a test when any lane
-    // needs it): usually one; a second near an edge shared by two candidate
-    // quads or behind a candidate whose bound was loose
-    {
-      const uint64_t k = pre_exact(lds_prex, k1, o, d);
-      // (a lane with o or d out of the margins' range, or no candidate -- it
-      // read record 31 -- ignores the result; the former scans every quad)
-      key = (lane_ok && k1 != ~0u) ? min(key, k) : key;
-    }
-    const bool need2 = lane_ok & ((k2 & ~31u) <= (uint32_t)(key >> 32));
-    if (__ballot(need2)) {
-      const uint64_t k = pre_exact(lds_prex, k2, o, d);
-      key = need2 ? min(key, k) : key;
-    }
-    const bool need3 = lane_ok & ((k3 & ~31u) <= (uint32_t)(key >> 32));
-    if (__ballot(need3)) {
-      const uint64_t k = pre_exact(lds_prex, k3, o, d);
-      key = need3 ? min(key, k) : key;
-    }
-    full = !lane_ok || (k3 & ~31u) <= (uint32_t)(key >> 32);  // k3 = ~0u (none) never is
+    full = !lane_ok || (k2 & ~31u) <= (uint32_t)(key >> 32);  // k2 = ~0u (none) never is
   }
   if (full_out) *full_out = !pre ? 2u : full ? 1u : 0u;  // 2: prefilter off for this scene
   if (__ballot(full)) {
     if (full) {
       const int g0 = sc->kind_begin[0], g1 = sc->kind_begin[1], g2 = sc->kind_begin[2], g3 = sc->kind_begin[3],
-                g4 = sc->kind_begin[4], g5 = sc->kind_begin[5];
+                g4 = sc->kind_begin[4], g5 = sc->kind_begin[5], g6 = sc->kind_begin[6];
       u16v cur = quad_head(sc, g0);
       scan_kind_pf<1>(sc, g0, g1, o, d, key, cur);
       scan_kind_pf<2>(sc, g1, g2, o, d, key, cur);
@@ -532,10 +486,6 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
       scan_kind_pf<4>(sc, g3, g4, o, d, key, cur);
       scan_kind_pf<5>(sc, g4, g5, o, d, key, cur);
       scan_kind_pf<6>(sc, g5, g6, o, d, key, cur);
-      if (vert) {  // the prefiltered vertical faces too
-        scan_kind_pf<7>(sc, g6, g7, o, d, key, cur);
-        scan_kind_pf<8>(sc, g7, g8, o, d, key, cur);
-      }
     }
   }
   if (key != kNoHitKey) {
@@ -740,12 +690,9 @@ RTP_DEV int shade_hit(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed,
     float sum = 0;
     // 1/|gen| once: QuadPDFWorklet's rmag and both unit_vector(gen) below
     const float rg = rmag(gen);
-#ifndef RTP_BOUND_SKIP_PDF
-#define RTP_BOUND_SKIP_PDF 0  // (timing bounds only, wrong images: 1 no quad pdf, 2 no sphere pdf, 3 neither)
-#endif
-    if (!(RTP_BOUND_SKIP_PDF & 1)) sum += weight * quad_pdf_value(L, hp, gen, rg);
+    sum += weight * quad_pdf_value(L, hp, gen, rg);
     (void)randf(seed);
-    if (!(RTP_BOUND_SKIP_PDF & 2)) sum += weight * sphere_pdf_value(L, hp, gen, sph_ctm);
+    sum += weight * sphere_pdf_value(L, hp, gen, sph_ctm);
     // PDFCosineWorklet (ScatterWorklet.h:96-112): mixture in double
     const f3 ug = scl(gen, rg);       // unit_vector(gen)
     const f3 w_hn = unit_vector(hn);  // build_from_w(hn).w (u and v are unused here)

@@ -168,19 +168,18 @@ struct alignas(16) PreQuad {
 };
 static_assert(sizeof(PreQuad) == 32, "the prefilter scan reads a PreQuad as one s_load_dwordx8");
 
-// Vertical face of a box rotated about y (kinds 7 and 8: one edge along y,
-// the other in the xz-plane; an exact parallelogram whose four vertices share
-// their x, z pairwise and their y pairwise, bit for bit): the face's plane
-// nx x + nz z = c with (nx, nz) a unit normal, and the face's extent about
-// (cu, cy) along e = (nz, -nx) and along y, widened outward on the host.
-// Read with uniform (scalar) loads, like PreQuad.
-struct alignas(16) PreVert {
-  float nx, nz, c;
-  float cu, ru;   // centre / half extent along e
-  float cy, ry;   // centre / half extent along y
-  int32_t qpos;   // position in DevScene::quads
+// The same quads for the prefilter's exact test in the plane's own axes:
+// e01 = b along axis i, e03 = c along axis j, a the third; s = +1 if
+// j == i+1 (mod 3) else -1 (the cross products' sign); the vertex v00 and
+// v11 coordinates permuted to (i, a, j).  Exact parallelograms only.
+struct alignas(16) PreExact {
+  float b, bs, c, cs;  // bs = s*b, cs = s*c
+  float vi, va, vj;    // v00
+  float wi, wa, wj;    // v11
+  int32_t i, s;
+  uint32_t key_lo;     // DevQuad::key_lo
+  int32_t pad[3];
 };
-static_assert(sizeof(PreVert) == sizeof(PreQuad), "pre[] holds both kinds of record");
 
 struct alignas(16) DevScene {
   int32_t n_quads;
@@ -203,18 +202,15 @@ struct alignas(16) DevScene {
   DevLights light;
   DevQuad quads[kMaxQuads];
   DevSphere spheres[kMaxSpheres];
-  // closest-hit prefilter over the axis-plane quads (groups 0..5 = kinds 1..6)
-  // and, when every one qualifies, the vertical faces of boxes rotated about y
-  // (groups 6, 7 = kinds 7, 8): n_pre == kind_begin[6] or kind_begin[8] when
-  // enabled, else 0; pre[] holds the axis quads grouped by plane axis,
-  // [pre_begin[a], pre_begin[a+1]), then the vertical faces (PreVert records)
-  // in [pre_begin[3], pre_begin[4]); pre_scale = max |vertex coordinate| of them
+  // closest-hit prefilter over the axis-plane quads (groups 0..5 = kinds 1..6):
+  // n_pre == kind_begin[6] when enabled, else 0; pre[] grouped by plane axis,
+  // [pre_begin[a], pre_begin[a+1]); pre_scale = max |vertex coordinate| of them
   int32_t n_pre;
-  int32_t pre_begin[5];
+  int32_t pre_begin[4];
   float pre_scale;
-  int32_t pad2[1];
+  int32_t pad2[2];
   PreQuad pre[kMaxPre];
-  QuadGeom prex[kMaxPre];  // by quad position (< n_pre): the scan heads, for the candidates' exact tests
+  PreExact prex[kMaxPre];  // by quad position (< n_pre)
   const uint32_t* cnodes;    // 8 * n_nodes compact nodes (4 words each; kCBvhSphereBit above)
   const int32_t* cidx;       // 8 * n_nodes: a sphere leaf's scene index (else -1)
   // the LDS walk's tree (kLdsWalkLeaf): global copies, loaded into each block's LDS
@@ -235,7 +231,7 @@ static_assert(offsetof(DevScene, spheres) == offsetof(DevScene, quads) + sizeof(
                   sizeof(DevSphere) * kMaxSpheres >= 2 * sizeof(DevQuad),
               "quads[] is followed by at least two quads' worth of DevScene");
 static_assert(offsetof(DevScene, prex) == offsetof(DevScene, pre) + sizeof(PreQuad) * kMaxPre &&
-                  sizeof(QuadGeom) * kMaxPre >= 2 * sizeof(PreQuad),
+                  sizeof(PreExact) * kMaxPre >= 2 * sizeof(PreQuad),
               "pre[] is followed by at least two records' worth of DevScene");
 
 // camera constants (Camera.cxx:437-474): eye, nlook, delta_x, delta_y
