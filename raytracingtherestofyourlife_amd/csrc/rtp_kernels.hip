@@ -40,10 +40,16 @@
 #define RTP_FF_MARGIN 12  // pool kernel: fast-forward when READY holds fewer than idle lanes + this
 #endif
 // history rows of a finished sample loaded together in the fast-forward batch
-constexpr int kHistPrefetch = 6;
+#ifndef RTP_HIST_PREFETCH
+#define RTP_HIST_PREFETCH 6
+#endif
+constexpr int kHistPrefetch = RTP_HIST_PREFETCH;
 // and the rest kHistChunk at a time (r03r: 4 rows per wait, -0.4% at N = 1,
 // -1.1% at the 1/8 share, against two per wait)
-constexpr int kHistChunk = 4;
+#ifndef RTP_HIST_CHUNK
+#define RTP_HIST_CHUNK 4
+#endif
+constexpr int kHistChunk = RTP_HIST_CHUNK;
 #ifndef RTP_WALK_DONE
 // pool kernel, sphere-BVH scenes: a loop iteration walks the BVH until this
 // many of the wave's paths have finished their walks (or all have)
