@@ -79,3 +79,29 @@ def test_hip_sample_shards_match_single_stream_statistically(device):
     st = sample_shard_consistency(single, shards, spp)
     assert_shards_consistent(st, "hip 256x144x2048")
     assert st["n"] > 0.99 * n
+
+
+def test_block_ttest_accepts_unbiased_and_rejects_biased_frames(oracle):
+    """shard.sample_shard_ttest, the check bench.py applies to its reduced C5
+    frame: on the oracle's 96x64 frame at 256 spp, the summed sample shards
+    (2 and 8 ranks) agree with the single stream (|t| <= 1); the same sum at
+    depth 2 instead of 20 does not (t = 14-22 when calibrated).  (A 5-10%
+    scaled frame reaches only t ~ 4 at this size: the block means' spread
+    grows with the scale; at bench.py's 65 536 pixels x 16 384 spp the
+    standard error is ~100x smaller.)"""
+    from raytracingtherestofyourlife_amd import shard
+
+    nx, ny, spp, depth = 96, 64, 256, 20
+    sc = oracle.cornell_box(0)
+    cam = oracle.camera_setup(nx, ny)
+    pix = np.arange(nx * ny, dtype=np.int64)
+    single = oracle.render_pixels(sc, cam, nx, ny, spp, depth, pix, nthreads=0)[0]
+    for G in (2, 8):
+        parts = [oracle.render_pixels(sc, cam, nx, ny, b.spp, depth, pix, seed_base=b.seed_base, nthreads=0)[0]
+                 for b in shard.sample_batches(spp, G, nx * ny)]
+        summed = np.sum(parts, axis=0)
+        st = shard.sample_shard_ttest(single, summed, spp)
+        assert shard.ttest_consistent(st) and st["t_max"] < 2.0, (G, st)
+    shallow = [oracle.render_pixels(sc, cam, nx, ny, b.spp, 2, pix, seed_base=b.seed_base, nthreads=0)[0]
+               for b in shard.sample_batches(spp, 2, nx * ny)]
+    assert not shard.ttest_consistent(shard.sample_shard_ttest(single, np.sum(shallow, axis=0), spp))
