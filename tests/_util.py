@@ -90,3 +90,15 @@ def assert_shards_consistent(st: dict, what: str = "") -> None:
     assert st["outliers"] < 0.08, f"{what}: {st['outliers']:.4f} of pixel channels beyond 5 sd: {st}"
     a, b = st["nan_single"], st["nan_sharded"]
     assert abs(a - b) <= 5 * np.sqrt(a + b) + 3, f"{what}: NaN pixel counts {a} vs {b}"
+
+
+def canonical_rgb_sha256(rgb) -> bytes:
+    """SHA-256 of float32 rgb sums with every NaN written as 0x7fc00000 (the
+    payload differs between x86 and CDNA), as tools/make_golden_digest.py
+    stores it for whole-frame digest fixtures."""
+    import hashlib
+
+    a = np.ascontiguousarray(rgb, dtype=np.float32).copy()
+    bits = a.view(np.uint32)
+    bits[np.isnan(a)] = 0x7FC00000
+    return hashlib.sha256(bits.astype("<u4").tobytes()).digest()

@@ -124,3 +124,52 @@ def test_c4_share_through_the_tile_instance(device, tables_on, rank, world):
     assert pix.size > g["pixels"].size // (2 * world)
     ok = same_bits_or_both_nan(rgba[pos, :3], g["rgb"][pix]).all(axis=1)
     assert ok.all(), f"{int((~ok).sum())} of {pix.size} golden pixels differ"
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(GOLD, "c4_full_digest.npz")),
+                    reason="tests/golden/c4_full_digest.npz not generated (tools/make_golden_digest.py)")
+@pytest.mark.parametrize("launch", ["contiguous", "tiles"])
+def test_c4_whole_frame_digest(device, tables_on, launch):
+    """The WHOLE C4 frame (1920x1080, 4096 spp, depth 50: 8.5e9 samples, the
+    tile shard's configuration) against the oracle's, every pixel: the
+    SHA-256 of the rgb sums (NaN canonical), the NaN pixel list, and -- for
+    the contiguous work-stealing launch, which carries them -- the digests of
+    the final seeds and live-bounce counts.  `tiles`: the tile instance every
+    rank of a C4 run launches (rank 0 of 1, clipped edge tiles rendered
+    whole), its in-canvas entries scattered (shard.tile_entries)."""
+    import torch
+
+    import raytracingtherestofyourlife_amd as rtp
+    from raytracingtherestofyourlife_amd import shard as sh
+
+    from _util import canonical_rgb_sha256, sha256_u32
+
+    g = _load("c4_full_digest")
+    nx, ny, spp, depth = int(g["nx"]), int(g["ny"]), int(g["spp"]), int(g["depth"])
+    n = nx * ny
+    cam = rtp.default_camera()
+    s = torch.cuda.current_stream().cuda_stream
+    if launch == "contiguous":
+        out = torch.empty((n, 4), dtype=torch.float32, device="cuda")
+        seeds = torch.empty(n, dtype=torch.int32, device="cuda")
+        live = torch.empty(n, dtype=torch.int32, device="cuda")
+        device.render_device(cam, nx, ny, spp, depth, out.data_ptr(), stream=s, seed_ptr=seeds.data_ptr(),
+                             live_ptr=live.data_ptr())
+        torch.cuda.synchronize()
+        rgb = out[:, :3].cpu().numpy()
+        sd, lv = seeds.cpu().numpy().view(np.uint32), live.cpu().numpy().view(np.uint32)
+        assert sha256_u32(sd) == bytes(g["seed_sha256"]), "final RNG states differ"
+        assert sha256_u32(lv) == bytes(g["live_sha256"]), "live-bounce counts differ"
+        assert int(lv.astype(np.uint64).sum()) == int(g["live_sum"])
+    else:
+        ent, pix = sh.tile_entries(nx, ny, 0, 1)
+        n_tiles = -(-nx // 16) * -(-ny // 16)
+        out = torch.empty((256 * n_tiles, 4), dtype=torch.float32, device="cuda")
+        device.render_tiles_device(cam, nx, ny, spp, depth, out.data_ptr(), 0, 1, stream=s)
+        torch.cuda.synchronize()
+        rgb = np.empty((n, 3), np.float32)
+        rgb[pix] = out[:, :3].cpu().numpy()[ent]
+    nan = np.flatnonzero(np.isnan(rgb).any(1))
+    assert np.array_equal(nan, g["nan_pixels"]), f"NaN pixels: {nan.size} vs {g['nan_pixels'].size}"
+    assert canonical_rgb_sha256(rgb) == bytes(g["rgb_sha256"]), (
+        f"rgb sums differ: channel sums {np.nansum(rgb.astype(np.float64), 0)} vs {g['rgb_sum']}")

@@ -1,0 +1,85 @@
+"""A whole-frame DIGEST fixture from the CPU oracle (test infrastructure):
+every pixel of a frame at full S x D, rendered in row chunks (resumable: each
+chunk's result is kept under --work until the frame is assembled), reduced
+to SHA-256 digests -- of the float32 rgb sums with every NaN written as one
+canonical pattern (NaN payloads differ between x86 and CDNA and carry no
+information), of the final seeds and of the live-bounce counts -- plus the
+NaN pixel list and float64 channel sums for diagnosis.  A render is bit-exact
+against the oracle iff its digests match.
+
+    python tools/make_golden_digest.py c4_full_digest 0 1920 1080 4096 50 [--threads 8]
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import oracle_ctypes as oc  # noqa: E402
+
+
+def canonical_rgb_bytes(rgb: np.ndarray) -> bytes:
+    a = np.ascontiguousarray(rgb, dtype=np.float32).copy()
+    bits = a.view(np.uint32)
+    bits[np.isnan(a)] = 0x7FC00000
+    return bits.astype("<u4").tobytes()
+
+
+def digest_fields(rgb: np.ndarray, seeds: np.ndarray, live: np.ndarray) -> dict:
+    rgb = np.asarray(rgb, np.float32)
+    return {"rgb_sha256": np.frombuffer(hashlib.sha256(canonical_rgb_bytes(rgb)).digest(), np.uint8),
+            "seed_sha256": np.frombuffer(hashlib.sha256(np.asarray(seeds).astype("<u4").tobytes()).digest(), np.uint8),
+            "live_sha256": np.frombuffer(hashlib.sha256(np.asarray(live).astype("<u4").tobytes()).digest(), np.uint8),
+            "nan_pixels": np.flatnonzero(np.isnan(rgb).any(1)).astype(np.int64),
+            "rgb_sum": np.nansum(rgb.astype(np.float64), axis=0),
+            "seed_sum": np.uint64(np.asarray(seeds).astype(np.uint64).sum()),
+            "live_sum": np.uint64(np.asarray(live).astype(np.uint64).sum())}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("name")
+    ap.add_argument("variant", type=int)
+    ap.add_argument("nx", type=int)
+    ap.add_argument("ny", type=int)
+    ap.add_argument("spp", type=int)
+    ap.add_argument("depth", type=int)
+    ap.add_argument("--threads", type=int, default=0)
+    ap.add_argument("--chunks", type=int, default=60)
+    ap.add_argument("--work", default="/tmp/rtp_golden_work")
+    a = ap.parse_args()
+    work = os.path.join(a.work, a.name)
+    os.makedirs(work, exist_ok=True)
+    sc = oc.cornell_box(a.variant)
+    cam = oc.camera_setup(a.nx, a.ny)
+    n = a.nx * a.ny
+    bounds = np.linspace(0, n, a.chunks + 1).astype(np.int64)
+    t0 = time.time()
+    for c in range(a.chunks):
+        f = os.path.join(work, f"chunk{c:04d}.npz")
+        if os.path.exists(f):
+            continue
+        pix = np.arange(bounds[c], bounds[c + 1], dtype=np.int64)
+        rgba, seeds, live = oc.render_pixels(sc, cam, a.nx, a.ny, a.spp, a.depth, pix, nthreads=a.threads)
+        np.savez(f + ".tmp.npz", rgb=rgba[:, :3], seeds=seeds, live=live)
+        os.replace(f + ".tmp.npz", f)
+        print(f"chunk {c + 1}/{a.chunks} ({pix.size} px): {time.time() - t0:.0f}s", flush=True)
+    parts = [np.load(os.path.join(work, f"chunk{c:04d}.npz")) for c in range(a.chunks)]
+    rgb = np.concatenate([p["rgb"] for p in parts])
+    seeds = np.concatenate([p["seeds"] for p in parts])
+    live = np.concatenate([p["live"] for p in parts])
+    out = os.path.join(ROOT, "tests", "golden", a.name + ".npz")
+    np.savez_compressed(out, variant=a.variant, nx=a.nx, ny=a.ny, spp=a.spp, depth=a.depth, camera=cam,
+                        **digest_fields(rgb, seeds, live))
+    print(f"{a.name}: {a.nx}x{a.ny} x {a.spp} spp x depth {a.depth}: L={live.sum() / (n * a.spp):.4f}, "
+          f"nan_px={int(np.isnan(rgb).any(1).sum())} -> {out}")
+
+
+if __name__ == "__main__":
+    main()
