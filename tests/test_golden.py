@@ -15,7 +15,7 @@ from _util import assert_render_equal, load_full_frame, rmse_normalized, same_bi
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 FULL_FRAMES = ["c2_full"]  # whole frames (byte-plane format, tools/make_golden.py full_frame_fixture)
 RENDERS = sorted(n for n in (os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLD, "*.npz")))
-                 if n not in FULL_FRAMES)
+                 if n not in FULL_FRAMES and not n.endswith("_digest"))  # (digest fixtures: test_gpu_fullsize)
 
 
 def _load(name):
@@ -163,3 +163,22 @@ def _c2_full_frame(device, path, g):
     ok = same_bits_or_both_nan(canvas[:, :3], g["rgb"]).all(1)
     assert ok.all(), f"{int((~ok).sum())} of {n} pixels differ, first {np.flatnonzero(~ok)[:8].tolist()}"
     assert rmse_normalized(canvas, np.c_[g["rgb"], np.zeros(n, np.float32)], 1000) < 1e-4
+
+
+def test_c4_full_digest_agrees_with_the_c4_subset():
+    """tests/golden/c4_full_digest.npz (tools/make_golden_digest.py: the whole
+    C4 frame from the oracle, as digests) and c4_subset16k.npz (16 384 of its
+    pixels in full) come from separate oracle runs: the subset's NaN pixels
+    are exactly the full frame's NaN pixels among them, and the configs agree."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    f = os.path.join(here, "golden", "c4_full_digest.npz")
+    if not os.path.exists(f):
+        pytest.skip("c4_full_digest.npz not generated")
+    full = np.load(f, allow_pickle=False)
+    sub = np.load(os.path.join(here, "golden", "c4_subset16k.npz"), allow_pickle=False)
+    for k in ("nx", "ny", "spp", "depth", "variant"):
+        assert int(full[k]) == int(sub[k]), k
+    assert np.array_equal(full["camera"], sub["camera"])
+    nan_sub = sub["pixels"][np.isnan(sub["rgb"]).any(1)]
+    assert np.array_equal(np.intersect1d(full["nan_pixels"], sub["pixels"]), np.sort(nan_sub))
+    assert full["rgb_sha256"].size == 32 and full["seed_sha256"].size == 32 and full["live_sha256"].size == 32

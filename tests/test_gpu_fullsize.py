@@ -145,6 +145,7 @@ def test_c4_whole_frame_digest(device, tables_on, launch):
     from _util import canonical_rgb_sha256, sha256_u32
 
     g = _load("c4_full_digest")
+    device.set_cornell_box(int(g["variant"]))
     nx, ny, spp, depth = int(g["nx"]), int(g["ny"]), int(g["spp"]), int(g["depth"])
     n = nx * ny
     cam = rtp.default_camera()
