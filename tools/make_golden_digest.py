@@ -8,6 +8,7 @@ NaN pixel list and float64 channel sums for diagnosis.  A render is bit-exact
 against the oracle iff its digests match.
 
     python tools/make_golden_digest.py c4_full_digest 0 1920 1080 4096 50 [--threads 8]
+    python tools/make_golden_digest.py c5_shard3_full_digest 0 3840 2160 2048 50 --seed-base 24883200
 """
 from __future__ import annotations
 
@@ -51,6 +52,7 @@ def main() -> None:
     ap.add_argument("spp", type=int)
     ap.add_argument("depth", type=int)
     ap.add_argument("--threads", type=int, default=0)
+    ap.add_argument("--seed-base", type=int, default=0, help="seed = pixel + seed_base (a sample-batch shard)")
     ap.add_argument("--chunks", type=int, default=60)
     ap.add_argument("--work", default="/tmp/rtp_golden_work")
     a = ap.parse_args()
@@ -66,7 +68,8 @@ def main() -> None:
         if os.path.exists(f):
             continue
         pix = np.arange(bounds[c], bounds[c + 1], dtype=np.int64)
-        rgba, seeds, live = oc.render_pixels(sc, cam, a.nx, a.ny, a.spp, a.depth, pix, nthreads=a.threads)
+        rgba, seeds, live = oc.render_pixels(sc, cam, a.nx, a.ny, a.spp, a.depth, pix, seed_base=a.seed_base,
+                                             nthreads=a.threads)
         np.savez(f + ".tmp.npz", rgb=rgba[:, :3], seeds=seeds, live=live)
         os.replace(f + ".tmp.npz", f)
         print(f"chunk {c + 1}/{a.chunks} ({pix.size} px): {time.time() - t0:.0f}s", flush=True)
@@ -76,6 +79,7 @@ def main() -> None:
     live = np.concatenate([p["live"] for p in parts])
     out = os.path.join(ROOT, "tests", "golden", a.name + ".npz")
     np.savez_compressed(out, variant=a.variant, nx=a.nx, ny=a.ny, spp=a.spp, depth=a.depth, camera=cam,
+                        seed_base=a.seed_base,
                         **digest_fields(rgb, seeds, live))
     print(f"{a.name}: {a.nx}x{a.ny} x {a.spp} spp x depth {a.depth}: L={live.sum() / (n * a.spp):.4f}, "
           f"nan_px={int(np.isnan(rgb).any(1).sum())} -> {out}")
