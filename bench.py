@@ -50,6 +50,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -235,6 +236,27 @@ def scaling_anchors(dev, cam, stream) -> dict:
     return out
 
 
+class Heartbeat:
+    """Rank 0 prints `bench: <phase> (<s> s)` to stderr every `period` seconds
+    (stdout keeps its one JSON line): a C5 run at N = 2 renders for minutes
+    between its start and its line, and a silent process looks hung."""
+
+    def __init__(self, enabled: bool, period: float = 30.0):
+        self.phase = "setup"
+        self.period = period
+        self.t0 = time.perf_counter()
+        self._stop = threading.Event()
+        if enabled:
+            threading.Thread(target=self._run, daemon=True).start()
+
+    def _run(self):
+        while not self._stop.wait(self.period):
+            print(f"bench: {self.phase} ({time.perf_counter() - self.t0:.0f} s)", file=sys.stderr, flush=True)
+
+    def stop(self):
+        self._stop.set()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -298,6 +320,7 @@ def main() -> None:
             setattr(args, k, W[k])
     if args.golden is None:
         args.golden = os.path.join(ROOT, "tests", "golden", W["golden"])
+    beat = Heartbeat(rank == 0)
     gpu = 0 if args.share_gpu else local
     torch.cuda.set_device(gpu)
     if world > 1 or args.force_collective:
@@ -390,6 +413,7 @@ def main() -> None:
 
     # (the first frame after setup is timed on one GPU only: at N > 1 a C5
     # frame takes seconds, and the warmup renders it anyway)
+    beat.phase = "first render and warmup"
     t_first = time.perf_counter()
     if world == 1:
         render()
@@ -407,6 +431,7 @@ def main() -> None:
     if grouped:
         dist.barrier()
     torch.cuda.synchronize()
+    beat.phase = f"{args.steps} timed steps"
     t0 = time.perf_counter()
     for k in range(args.steps):
         # kernel duration bracketed on the stream the kernel is launched on
@@ -422,6 +447,7 @@ def main() -> None:
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if args.steps else float("nan")
 
     # ---- after the timed region: checks and the same-workload one-GPU anchor ----
+    beat.phase = "checks and the one-GPU anchor"
     coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
     quality = None
     shard_exact = None
@@ -510,6 +536,7 @@ def main() -> None:
     # timed launch is contiguous, the contiguous launch when it is the tile
     # deal; the two render at rates within ~1%, r04q), so the rocprof
     # statistics of the timed instance stay the timed renders'.
+    beat.phase = "one-shot render and scaling anchors"
     off_ms = float("nan")
     if world == 1:
         dev.set_ff_tables("off")
@@ -569,6 +596,7 @@ def main() -> None:
     setup_base_ms = (t_scene - t_setup) * 1e3  # context + scene
     e2e_s = t_first_done - t_setup
 
+    beat.phase = "CPU baseline"
     if rank == 0:
         cpu = cpu_mt = None
         if world == 1 and args.cpu_budget > 0:
@@ -650,7 +678,9 @@ def main() -> None:
             line["shard_exact"] = shard_exact
         if check is not None:
             line["check_reduced_canvas" + ("" if samples else "_equals_single_render")] = check
+        beat.stop()
         print(json.dumps(line), flush=True)
+    beat.stop()
     if grouped:
         dist.destroy_process_group()
 
