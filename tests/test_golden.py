@@ -182,3 +182,26 @@ def test_c4_full_digest_agrees_with_the_c4_subset():
     nan_sub = sub["pixels"][np.isnan(sub["rgb"]).any(1)]
     assert np.array_equal(np.intersect1d(full["nan_pixels"], sub["pixels"]), np.sort(nan_sub))
     assert full["rgb_sha256"].size == 32 and full["seed_sha256"].size == 32 and full["live_sha256"].size == 32
+
+
+@pytest.mark.parametrize("name", ["c5_shard3_full_digest", "c5_shard3_band_digest"])
+def test_c5_share_digest_agrees_with_the_2048spp_fixture(name):
+    """A C5 rank-share digest (tools/make_golden_digest.py: rank 3 of 8's
+    share over the whole canvas or its leading band) and c5_shard3_2048spp.npz
+    (1024 of the share's pixels in full, bench.py's shard check) come from
+    separate oracle runs: same configuration, and among the fixture's pixels
+    inside the digest's range the NaN pixels are the same."""
+    f = os.path.join(GOLD, name + ".npz")
+    if not os.path.exists(f):
+        pytest.skip(f"{name}.npz not generated")
+    d = np.load(f, allow_pickle=False)
+    sub = _load("c5_shard3_2048spp")
+    for k in ("nx", "ny", "spp", "depth", "variant", "seed_base"):
+        assert int(d[k]) == int(sub[k]), k
+    assert np.array_equal(d["camera"], sub["camera"])
+    n = int(d["pixel_count"]) if "pixel_count" in d.files else int(d["nx"]) * int(d["ny"])
+    inside = sub["pixels"][sub["pixels"] < n]
+    assert inside.size > 0
+    nan_sub = sub["pixels"][np.isnan(sub["rgb"]).any(1) & (sub["pixels"] < n)]
+    assert np.array_equal(np.intersect1d(d["nan_pixels"], inside), np.sort(nan_sub))
+    assert d["nan_pixels"].size == 0 or int(d["nan_pixels"].max()) < n

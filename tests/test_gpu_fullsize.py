@@ -176,13 +176,19 @@ def test_c4_whole_frame_digest(device, tables_on, launch):
         f"rgb sums differ: channel sums {np.nansum(rgb.astype(np.float64), 0)} vs {g['rgb_sum']}")
 
 
-@pytest.mark.skipif(not os.path.exists(os.path.join(GOLD, "c5_shard3_full_digest.npz")),
-                    reason="tests/golden/c5_shard3_full_digest.npz not generated (tools/make_golden_digest.py)")
-def test_c5_rank_share_whole_canvas_digest(device, tables_on):
-    """Rank 3 of 8's whole share of the C5 frame (3840x2160, 2048 of 16384
-    spp on the derived stream seed = pixel + 3 * 8294400: 1.7e10 samples,
-    what bench.py's rank 3 renders per step at N = 8) against the oracle's
-    digests: rgb sums (NaN canonical), NaN pixels, final seeds, live counts."""
+C5_DIGESTS = [n for n in ("c5_shard3_full_digest", "c5_shard3_band_digest")
+              if os.path.exists(os.path.join(GOLD, n + ".npz"))][:1]  # the whole canvas when generated
+
+
+@pytest.mark.skipif(not C5_DIGESTS, reason="no C5 share digest generated (tools/make_golden_digest.py)")
+@pytest.mark.parametrize("name", C5_DIGESTS)
+def test_c5_rank_share_whole_canvas_digest(device, tables_on, name):
+    """Rank 3 of 8's share of the C5 frame (3840x2160, 2048 of 16384 spp on
+    the derived stream seed = pixel + 3 * 8294400: what bench.py's rank 3
+    renders per step at N = 8) against the oracle's digests over the
+    fixture's pixels -- the whole canvas (1.7e10 samples), or its leading band
+    of rows (`pixel_count`, tools/make_golden_digest.py --assemble-first) --:
+    rgb sums (NaN canonical), NaN pixels, final seeds, live counts."""
     import torch
 
     import raytracingtherestofyourlife_amd as rtp
@@ -190,16 +196,17 @@ def test_c5_rank_share_whole_canvas_digest(device, tables_on):
 
     from _util import canonical_rgb_sha256, sha256_u32
 
-    g = _load("c5_shard3_full_digest")
+    g = _load(name)
     device.set_cornell_box(int(g["variant"]))
     nx, ny, spp, depth, sb = int(g["nx"]), int(g["ny"]), int(g["spp"]), int(g["depth"]), int(g["seed_base"])
     b = sh.sample_batches(16384, 8, nx * ny)[3]
     assert (b.spp, b.seed_base) == (spp, sb)  # the bench's rank 3 of 8
-    n = nx * ny
+    n = int(g.get("pixel_count", nx * ny))
+    assert int(g.get("pixel_begin", 0)) == 0
     out = torch.empty((n, 4), dtype=torch.float32, device="cuda")
     seeds = torch.empty(n, dtype=torch.int32, device="cuda")
     live = torch.empty(n, dtype=torch.int32, device="cuda")
-    device.render_device(rtp.default_camera(), nx, ny, spp, depth, out.data_ptr(), seed_base=sb,
+    device.render_device(rtp.default_camera(), nx, ny, spp, depth, out.data_ptr(), pixel_count=n, seed_base=sb,
                          stream=torch.cuda.current_stream().cuda_stream, seed_ptr=seeds.data_ptr(),
                          live_ptr=live.data_ptr())
     torch.cuda.synchronize()

@@ -9,6 +9,11 @@ against the oracle iff its digests match.
 
     python tools/make_golden_digest.py c4_full_digest 0 1920 1080 4096 50 [--threads 8]
     python tools/make_golden_digest.py c5_shard3_full_digest 0 3840 2160 2048 50 --seed-base 24883200
+
+A second process can share the work: --reverse-from C renders chunks C-1
+down to 0 (both skip chunks already kept).  --assemble-first K writes the
+digest of the first K chunks only (pixels [0, bounds[K]): a leading band of
+the frame, its pixel_count recorded) once those exist.
 """
 from __future__ import annotations
 
@@ -55,6 +60,8 @@ def main() -> None:
     ap.add_argument("--seed-base", type=int, default=0, help="seed = pixel + seed_base (a sample-batch shard)")
     ap.add_argument("--chunks", type=int, default=60)
     ap.add_argument("--work", default="/tmp/rtp_golden_work")
+    ap.add_argument("--reverse-from", type=int, default=None, help="render chunks C-1 .. 0 (a helper process)")
+    ap.add_argument("--assemble-first", type=int, default=None, help="assemble the first K chunks only")
     a = ap.parse_args()
     work = os.path.join(a.work, a.name)
     os.makedirs(work, exist_ok=True)
@@ -63,7 +70,10 @@ def main() -> None:
     n = a.nx * a.ny
     bounds = np.linspace(0, n, a.chunks + 1).astype(np.int64)
     t0 = time.time()
-    for c in range(a.chunks):
+    order = range(a.chunks) if a.reverse_from is None else range(a.reverse_from - 1, -1, -1)
+    if a.assemble_first is not None:
+        order = []
+    for c in order:
         f = os.path.join(work, f"chunk{c:04d}.npz")
         if os.path.exists(f):
             continue
@@ -73,15 +83,20 @@ def main() -> None:
         np.savez(f + ".tmp.npz", rgb=rgba[:, :3], seeds=seeds, live=live)
         os.replace(f + ".tmp.npz", f)
         print(f"chunk {c + 1}/{a.chunks} ({pix.size} px): {time.time() - t0:.0f}s", flush=True)
-    parts = [np.load(os.path.join(work, f"chunk{c:04d}.npz")) for c in range(a.chunks)]
+    k = a.chunks if a.assemble_first is None else a.assemble_first
+    missing = [c for c in range(k) if not os.path.exists(os.path.join(work, f"chunk{c:04d}.npz"))]
+    if missing:
+        raise SystemExit(f"{len(missing)} chunks still missing (first {missing[:4]})")
+    parts = [np.load(os.path.join(work, f"chunk{c:04d}.npz")) for c in range(k)]
     rgb = np.concatenate([p["rgb"] for p in parts])
     seeds = np.concatenate([p["seeds"] for p in parts])
     live = np.concatenate([p["live"] for p in parts])
     out = os.path.join(ROOT, "tests", "golden", a.name + ".npz")
     np.savez_compressed(out, variant=a.variant, nx=a.nx, ny=a.ny, spp=a.spp, depth=a.depth, camera=cam,
-                        seed_base=a.seed_base,
+                        seed_base=a.seed_base, pixel_begin=0, pixel_count=int(bounds[k]),
                         **digest_fields(rgb, seeds, live))
-    print(f"{a.name}: {a.nx}x{a.ny} x {a.spp} spp x depth {a.depth}: L={live.sum() / (n * a.spp):.4f}, "
+    print(f"{a.name}: {a.nx}x{a.ny} ({int(bounds[k])} px) x {a.spp} spp x depth {a.depth}: "
+          f"L={live.sum() / (int(bounds[k]) * a.spp):.4f}, "
           f"nan_px={int(np.isnan(rgb).any(1).sum())} -> {out}")
 
 
