@@ -210,7 +210,6 @@ def sample_shard_consistency(single: np.ndarray, shards: list, spp: int) -> dict
     }
 
 
-
 def sample_shard_ttest(single: np.ndarray, shards_sum: np.ndarray, spp: int, blocks: int = 256) -> dict:
     """Frame-level test that a sample-sharded image (shards_sum: the G shards'
     sums, spp samples per pixel in all) and the single-stream image of the
