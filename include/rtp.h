@@ -255,8 +255,12 @@ rtp_status rtp_eval_powf(rtp_context* ctx, const float* x, float y, float* out, 
  *                       past its break-even count (setup time / time saved
  *                       per sample): the chain tables (64 GiB) at
  *                       auto_samples, the direct tables at
- *                       auto_samples_direct.  A one-shot render such as
- *                       main.cc's never pays the setup
+ *                       auto_samples_direct (once the chain tables exist:
+ *                       their sample count + the direct stage's estimated
+ *                       setup -- 0.07 s + 2.5x the chain tables' measured
+ *                       allocation -- over the time it saves per sample).
+ *                       A one-shot render such as main.cc's never pays the
+ *                       setup
  *   RTP_FF_TABLES_OFF   hash every dead depth on this context
  *   RTP_FF_TABLES_ON    build now (a long-lived renderer / service)
  * Environment: RTP_FF_POLICY=auto|on|off sets the default of new contexts. */

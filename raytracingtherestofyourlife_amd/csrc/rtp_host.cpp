@@ -224,6 +224,8 @@ struct FfTables {
   int d_first = 0, d_count = 0, n_chain = 0;
   int stage = 0;  // built so far: 1 chain tables, 2 + direct tables
   double alloc_ms = 0, build_ms = 0;
+  double chain_alloc_ms = -1;  // the chain stage's own allocation time (-1: not built)
+  uint64_t chain_at = 0;       // samples_seen when the chain stage was built
   uint64_t bytes = 0;
   uint64_t samples_seen = 0;  // samples launched on this device (the AUTO policy's count)
 };
@@ -239,21 +241,34 @@ int ff_policy_default() {
 
 // AUTO builds in two stages, each once the samples launched on the device
 // (this launch included) reach its break-even count: setup time over the
-// kernel time it saves per sample (C2 on MI355X, profiles/r03b_*):
-//  - chain tables (64 GiB): ~0.25 s setup, 147 -> 125 ms per 6.4e8 samples
-//    (3.4e-11 s/sample): 7.4e9 samples, ~12 C2 renders;
-//  - direct tables (+160 GiB): 2.5-5 s of allocation (the driver clears the
-//    memory) + 0.2 s build, 125 -> 117 ms (1.3e-11 s/sample): ~3e11
-//    samples, ~450 C2 renders.
-// RTP_FF_AUTO_SAMPLES=chain[,direct] overrides.
-void ff_auto_samples(uint64_t& chain, uint64_t& direct) {
+// kernel time it saves per sample (C2 on MI355X; round 5,
+// profiles/r05z_ff_policy.txt: no tables 126.0 ms, chain tables 106.8 ms,
+// all 98.9 ms per 6.4e8 samples):
+//  - chain tables (64 GiB): 0.12 s build + an allocation that takes 1 ms to
+//    ~1.5 s depending on the box (the driver clearing the memory), saving
+//    3.0e-11 s/sample: 7.5e9 samples, ~12 C2 renders (allows ~0.1 s of
+//    allocation);
+//  - direct tables (+160 GiB): 0.07 s more build + 2.5x the chain stage's
+//    measured allocation time, saving 1.23e-11 s/sample: counted from the
+//    chain stage, ~9 C2 renders where allocation is fast, ~450 where the
+//    chain's 64 GiB took 1.4 s; 3e11 samples before the chain stage is built.
+// RTP_FF_AUTO_SAMPLES=chain[,direct] overrides (absolute counts).
+constexpr double kFfChainSavePerSample = 3.0e-11, kFfDirectSavePerSample = 1.23e-11;
+constexpr double kFfDirectBuildS = 0.07, kFfDirectAllocRatio = 160.0 / 64.0;
+void ff_auto_samples(uint64_t& chain, uint64_t& direct, const FfTables* T = nullptr) {
   chain = 7500000000ull;
   direct = 300000000000ull;
   if (const char* e = getenv("RTP_FF_AUTO_SAMPLES")) {
     char* end = nullptr;
     chain = std::strtoull(e, &end, 10);
     direct = (end && *end == ',') ? std::strtoull(end + 1, nullptr, 10) : chain;
+    return;
   }
+  if (T && T->chain_alloc_ms >= 0) {
+    const double setup_s = kFfDirectBuildS + kFfDirectAllocRatio * T->chain_alloc_ms / 1e3;
+    direct = std::min<uint64_t>(direct, T->chain_at + (uint64_t)(setup_s / kFfDirectSavePerSample));
+  }
+  (void)kFfChainSavePerSample;
 }
 
 // Allocate and build the tables of a device up to `stage` (caller holds
@@ -309,7 +324,12 @@ void ff_build(FfTables& T, int stage) {
     }
   }
   (void)hipGetLastError();
-  T.alloc_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  const double alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  T.alloc_ms += alloc_ms;
+  if (T.stage < 1 && stage == 1 && n_chain > 0) {  // the AUTO policy's estimate of the direct stage's cost
+    T.chain_alloc_ms = alloc_ms;
+    T.chain_at = T.samples_seen;
+  }
   T.stage = stage;  // (a failed stage is not retried)
   if (max_r > 0) {
     const uint32_t t1 = which_threshold(2), t2 = which_threshold(3);
@@ -361,7 +381,7 @@ FfSnap ff_tables(int device, int policy, uint64_t samples) {
     ff_build(T, 2);
   } else if (policy == RTP_FF_TABLES_AUTO) {
     uint64_t chain = 0, direct = 0;
-    ff_auto_samples(chain, direct);
+    ff_auto_samples(chain, direct, &T);
     if (T.samples_seen >= direct) ff_build(T, 2);
     else if (T.samples_seen >= chain) ff_build(T, 1);
   }
@@ -1411,7 +1431,7 @@ rtp_status rtp_get_ff_tables(rtp_context* c, rtp_ff_info* out) {
   out->build_ms = T.build_ms;
   out->samples_seen = T.samples_seen;
   uint64_t chain = 0, direct = 0;
-  ff_auto_samples(chain, direct);
+  ff_auto_samples(chain, direct, &T);
   out->auto_samples = chain;
   out->auto_samples_direct = direct;
   return RTP_OK;
