@@ -205,3 +205,16 @@ def test_c5_share_digest_agrees_with_the_2048spp_fixture(name):
     nan_sub = sub["pixels"][np.isnan(sub["rgb"]).any(1) & (sub["pixels"] < n)]
     assert np.array_equal(np.intersect1d(d["nan_pixels"], inside), np.sort(nan_sub))
     assert d["nan_pixels"].size == 0 or int(d["nan_pixels"].max()) < n
+
+
+def test_c5_band_digest_is_the_full_digests_leading_band():
+    """The band fixture (the first 1080 rows) and the whole-canvas fixture
+    come from the same oracle chunks: their NaN pixels agree on the band."""
+    fs = [os.path.join(GOLD, n + ".npz") for n in ("c5_shard3_full_digest", "c5_shard3_band_digest")]
+    if not all(os.path.exists(f) for f in fs):
+        pytest.skip("C5 share digests not generated")
+    full, band = (np.load(f, allow_pickle=False) for f in fs)
+    n = int(band["pixel_count"])
+    assert n == int(full["nx"]) * int(full["ny"]) // 2
+    assert np.array_equal(full["nan_pixels"][full["nan_pixels"] < n], band["nan_pixels"])
+    assert int(band["live_sum"]) < int(full["live_sum"])
