@@ -35,9 +35,14 @@ and RNG jump tables are set up before the timed region -- `setup` and
 `first_render_ms` report what that costs, and `one_shot` what a fresh process
 rendering once, like main.cc, would see).  `rmse` / `bit_exact` compare the
 last timed frame (normalised, NormalizeFunctor) with the oracle's committed
-C2 frame (tests/golden/c2_full.npz); C5 checks a rank's shard against the
-committed c5_shard3_2048spp fixture (bit-exact) and the reduced frame against
-the single-stream image statistically.  `roofline` prices the render kernel
+C2 frame (tests/golden/c2_full.npz); at N > 1 the C5 line takes them from
+`reduced_frame_parity`: every rank's shard and the reduced frame at 1024
+pixels against the oracle's reduced-frame fixture of that N
+(tests/golden/c5_reduced.npz, N = 2/4/8; bit-exact shards, the reduced frame
+bit-exact against the shards' sum in the reduce's association), plus the
+statistical check of the reduced frame against an independent single-stream
+image.  `bench.py --gpus N` without torch.distributed.run starts it (one
+process per GPU) as a child and relays rank 0's line.  `roofline` prices the render kernel
 with the SoA byte model of SURVEY.md 8(d) (56 + 88*L bytes per sample) against
 the 8 TB/s HBM peak; `roofline_valu` gives the VALU-issue bound (the one that
 binds) from the committed PMC summary; `cpu_baseline` times
@@ -67,7 +72,7 @@ WORKLOADS = {
            "name": "C2: Cornell Box 800x800, 1000 spp, depth 50"},
     "c4": {"nx": 1920, "ny": 1080, "spp": 4096, "depth": 50, "golden": "c4_subset16k.npz",
            "name": "C4: Cornell Box 1920x1080, 4096 spp, depth 50 (BASELINE configs[3], image-tile shard)"},
-    "c5": {"nx": 3840, "ny": 2160, "spp": 16384, "depth": 50, "golden": "c5_shard3_2048spp.npz",
+    "c5": {"nx": 3840, "ny": 2160, "spp": 16384, "depth": 50, "golden": "c5_reduced.npz",
            "name": "C5: Cornell Box 3840x2160, 16384 spp, depth 50 (BASELINE configs[4], sample-batch shard)"},
 }
 SHARD = {"c2": "tiles", "c4": "tiles", "c5": "samples"}
@@ -165,6 +170,118 @@ def frame_quality(canvas: np.ndarray, gold: dict, spp: int) -> dict:
     return {"rmse": float(np.sqrt(np.mean(d * d))), "bit_exact": bool(same.all()),
             "pixels_checked": int(len(b)), "pixels_differing": int((~same.all(1)).sum()),
             "nan_pixels_ref": int(np.isnan(gold["rgb"]).any(1).sum())}
+
+
+def launch_cmd(argv: list, gpus: int, port: int) -> list:
+    """`bench.py --gpus N` started without torch.distributed.run (WORLD_SIZE
+    unset): the one-process-per-GPU launch of the driver's contract, as a
+    fresh child process started before this process touches the GPU."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def self_launch(argv: list, gpus: int) -> int:
+    """Run launch_cmd as a child (stdout inherited: rank 0's JSON line is this
+    process's line) and return its exit code."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(launch_cmd(argv, gpus, port), env=env).returncode
+
+
+REDUCED_FIXTURES = ("c5_reduced.npz", "c5_reduced_small.npz")
+
+
+def find_reduced_fixture(nx: int, ny: int, spp: int, depth: int, world: int, explicit: str | None = None):
+    """The oracle's reduced-frame fixture (tools/make_golden_reduced.py) of
+    this sample-shard configuration and world size: every rank's shard at the
+    fixture pixels (shards_N [N, n, 3]) and their float32 sum in rank order
+    (reduced_N); None if no committed fixture matches."""
+    cands = [explicit] if explicit else [os.path.join(ROOT, "tests", "golden", f) for f in REDUCED_FIXTURES]
+    for path in cands:
+        try:
+            z = np.load(path, allow_pickle=False)
+        except (OSError, ValueError):
+            continue
+        if f"shards_{world}" not in z.files:
+            continue
+        if (int(z["nx"]), int(z["ny"]), int(z["spp"]), int(z["depth"])) != (nx, ny, spp, depth):
+            continue
+        return {"name": os.path.basename(path), "pixels": np.asarray(z["pixels"], np.int64),
+                "shards": np.asarray(z[f"shards_{world}"], np.float32),
+                "reduced": np.asarray(z[f"reduced_{world}"], np.float32)}
+    return None
+
+
+def _same_bits(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    return (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+
+
+def association_sums(shards: np.ndarray) -> dict:
+    """float32 sums of the N shards in the associations a reduce may use: a
+    chain along the ring of ranks from any start k, in either direction
+    (((s_k + s_k+1) + ...) + s_k-1: a ring reduce, and a ring reduce-scatter
+    whose chunk c starts at rank c + 1 -- gloo, or RCCL's channels), and the
+    pairwise tree.  "rank_order" is the forward chain from rank 0."""
+    s = [np.asarray(x, np.float32) for x in shards]
+    n = len(s)
+    if n <= 2:  # one add: the same either way
+        return {"rank_order": s[0] + s[1] if n == 2 else s[0].copy()}
+    out = {}
+    for direction in (1, -1):
+        for k in range(n):
+            order = [(k + direction * i) % n for i in range(n)]
+            acc = s[order[0]].copy()
+            for r in order[1:]:
+                acc = acc + s[r]
+            name = "rank_order" if (direction, k) == (1, 0) else f"ring_{'fwd' if direction > 0 else 'rev'}_from_{k}"
+            out[name] = acc
+    lvl = s
+    while len(lvl) > 1:
+        lvl = [lvl[i] + lvl[i + 1] if i + 1 < len(lvl) else lvl[i] for i in range(0, len(lvl), 2)]
+    out["pairwise_tree"] = lvl[0]
+    return out
+
+
+def reduced_frame_parity(fix: dict, shards_got: list, reduced_got: np.ndarray, spp: int) -> dict:
+    """The N > 1 line's parity against the oracle:
+    every rank's shard at the fixture pixels bit for bit against the oracle's
+    shard, and the reduced frame against the oracle's reduced frame -- bit for
+    bit against the oracle shards' float32 sum in some association a reduce
+    may use (two ranks: one add, so exactly the fixture), and the per-pixel
+    RMSE of the normalised frames (NormalizeFunctor, main.cc:253-287) against
+    the fixture's rank-order sum.  shards_got: N arrays [n, >=3]; reduced_got
+    [n, >=3]."""
+    import raytracingtherestofyourlife_amd as rtp
+
+    want = fix["shards"]
+    n = want.shape[1]
+    shard_ok = [bool(_same_bits(np.ascontiguousarray(g[:, :3], np.float32), w).all())
+                for g, w in zip(shards_got, want)]
+    red = np.ascontiguousarray(reduced_got[:, :3], np.float32)
+    sums = association_sums(want)
+    per = {k: _same_bits(red, v).all(1) for k, v in sums.items()}
+    any_match = np.logical_or.reduce(list(per.values()))
+    a = np.c_[red, np.zeros(n, np.float32)].astype(np.float32)
+    b = np.c_[fix["reduced"], np.zeros(n, np.float32)].astype(np.float32)
+    rtp.normalize(a, spp)
+    rtp.normalize(b, spp)
+    d = a[:, :3].astype(np.float64) - b[:, :3].astype(np.float64)
+    fin = np.isfinite(red) & np.isfinite(fix["reduced"])
+    rel = np.abs(red[fin].astype(np.float64) - fix["reduced"][fin]) / np.maximum(np.abs(fix["reduced"][fin]), 1e-30)
+    return {"fixture": fix["name"], "pixels": int(n), "ranks": len(want),
+            "shards_bit_exact": all(shard_ok) and len(shard_ok) == len(want),
+            "shard_bit_exact_per_rank": shard_ok,
+            "reduced_bit_exact_rank_order": bool(per["rank_order"].all()),
+            "reduced_association": {k: int(v.sum()) for k, v in per.items()},
+            "reduced_pixels_matching_an_association": int(any_match.sum()),
+            "reduced_max_rel_vs_rank_order": float(rel.max()) if rel.size else 0.0,
+            "rmse": float(np.sqrt(np.mean(d * d))),
+            "bit_exact": bool(all(shard_ok) and any_match.all())}
 
 
 def load_valu(path: str, cfg: dict, kernel_ms: float):
@@ -300,6 +417,10 @@ def main() -> None:
                          "(rtp_render_device over [0, nx*ny), like main.cc's render); tiles = the tile-deal instance "
                          "the ranks of an N-GPU run use (rank 0 of 1)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: torch.distributed.run as a fresh child, before
+        # anything here touches the GPU; never a one-GPU line for --gpus N
+        raise SystemExit(self_launch(sys.argv[1:], args.gpus))
 
     import torch
     import torch.distributed as dist
@@ -310,7 +431,7 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
+    if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     workload = args.workload if args.workload != "auto" else ("c2" if world == 1 else "c5")
     W = WORKLOADS[workload]
@@ -318,6 +439,7 @@ def main() -> None:
     for k in ("nx", "ny", "spp", "depth"):
         if getattr(args, k) is None:
             setattr(args, k, W[k])
+    golden_given = args.golden is not None
     if args.golden is None:
         args.golden = os.path.join(ROOT, "tests", "golden", W["golden"])
     beat = Heartbeat(rank == 0)
@@ -450,28 +572,24 @@ def main() -> None:
     beat.phase = "checks and the one-GPU anchor"
     coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
     quality = None
-    shard_exact = None
+    parity = None
     gathered = None
     if samples:
-        # (a) a rank whose batch is a committed fixture's (c5_shard3_2048spp:
-        # rank 3 of 8) compares its own last shard with it, bit for bit
-        code = torch.tensor([-1], dtype=torch.int64)
-        g = load_golden_frame(args.golden, any_seed=True)
-        if g and g["pixels"] is not None and (g["nx"], g["ny"], g["spp"], g["depth"], g["seed_base"]) == (
-                nx, ny, spp_mine, args.depth, seed_base):
-            part = out.index_select(0, torch.from_numpy(g["pixels"]).cuda())[:, :3].cpu().numpy()
-            same = (part.view(np.uint32) == g["rgb"].view(np.uint32)) | (np.isnan(part) & np.isnan(g["rgb"]))
-            code[0] = 1 if same.all() else 0
-        codes = [torch.zeros(1, dtype=torch.int64, device=coll_dev) for _ in range(world)]
-        if grouped:
-            dist.all_gather(codes, code.to(coll_dev))
-        else:
-            codes = [code]
-        hit = [r for r in range(world) if int(codes[r].item()) >= 0]
-        if hit:
-            shard_exact = {"fixture": os.path.basename(args.golden), "rank": hit[0],
-                           "pixels": int(g["rgb"].shape[0]) if g else None,
-                           "bit_exact": all(int(codes[r].item()) == 1 for r in hit)}
+        # (a) every rank's shard at the pixels of the oracle's reduced-frame
+        # fixture of this world size (tools/make_golden_reduced.py), gathered
+        # to rank 0 with the reduced frame there (reduced_frame_parity)
+        fix = find_reduced_fixture(nx, ny, args.spp, args.depth, world,
+                                   args.golden if golden_given else None)
+        if fix is not None:
+            mine = out.index_select(0, torch.from_numpy(fix["pixels"]).cuda()).to(coll_dev)
+            if grouped and world > 1:
+                parts = [torch.empty_like(mine) for _ in range(world)]
+                dist.all_gather(parts, mine)
+            else:
+                parts = [mine]
+            if rank == 0:
+                red_px = canvas.index_select(0, torch.from_numpy(fix["pixels"]).cuda()).cpu().numpy()
+                parity = reduced_frame_parity(fix, [q.cpu().numpy() for q in parts], red_px, args.spp)
         # (b) every rank's shard at a fixed pixel sample, gathered to rank 0
         # for the statistical comparison with the single-stream image
         chk = np.sort(np.random.default_rng(5).choice(nx * ny, min(C5_CHECK_PIXELS, nx * ny), replace=False))
@@ -489,16 +607,24 @@ def main() -> None:
     if rank == 0 and (want_anchor or args.check):
         # rank 0 renders the same workload's whole frame alone: the one-GPU
         # time of this workload (the others wait at the barrier below)
+        # sample batches: the anchor renders on a stream no rank uses
+        # (seed_base N*nx*ny), so the statistical check compares two
+        # independent estimates (rank 0's batch IS the first spp/N samples of
+        # the seed_base-0 stream)
+        anchor_seed = (world * nx * ny) & 0xFFFFFFFF if samples else 0
         full = torch.empty((nx * ny, 4), dtype=torch.float32, device="cuda")
-        st = dev.render_device(cam, nx, ny, args.spp, args.depth, full.data_ptr(), stream=stream.cuda_stream,
-                               timed=True)
         torch.cuda.synchronize()
+        t_one = time.perf_counter()
+        st = dev.render_device(cam, nx, ny, args.spp, args.depth, full.data_ptr(), seed_base=anchor_seed,
+                               stream=stream.cuda_stream, timed=True)
+        torch.cuda.synchronize()
+        one_wall_ms = (time.perf_counter() - t_one) * 1e3
         one_ms = float(st.kernel_ms)
-        one_gpu = {"kernel_ms": round(one_ms, 2),
+        one_gpu = {"kernel_ms": round(one_ms, 2), "wall_ms": round(one_wall_ms, 2),
                    "msamples_per_s": round(nx * ny * args.spp / one_ms / 1e3, 1),
                    "launch": "rank 0's GPU alone, the whole frame through the default contiguous launch"
-                             + (" on the single stream (seed_base 0: the N = 1 schedule; same pixels, samples "
-                                "and scene as the sharded frame)" if samples else "")}
+                             + (f" on a stream no rank uses (seed_base {anchor_seed}; same pixels, samples and "
+                                f"scene as the sharded frame)" if samples else "")}
         red_np = canvas[:, :3].cpu().numpy()
         if samples:
             single = full.index_select(0, torch.from_numpy(chk).cuda()).cpu().numpy()
@@ -560,13 +686,15 @@ def main() -> None:
         gold = load_golden_frame(args.golden)
         if gold and (gold["nx"], gold["ny"], gold["spp"], gold["depth"]) == (nx, ny, args.spp, args.depth):
             quality = frame_quality(canvas.cpu().numpy(), gold, args.spp)
+    kernel_ms_max = kernel_ms
     if grouped:
-        t = torch.tensor([elapsed, live_total], dtype=torch.float64, device=coll_dev)
+        t = torch.tensor([elapsed, live_total, kernel_ms], dtype=torch.float64, device=coll_dev)
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         tot = t.clone()
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         elapsed = float(mx[0].item())
+        kernel_ms_max = float(mx[2].item())
         live_all = float(tot[1].item())
     else:
         live_all = float(live_total)
@@ -638,8 +766,10 @@ def main() -> None:
                 "live_bounces_per_sample": round(L, 6),
                 "dist_backend": args.dist_backend if grouped else None,
             },
-            "rmse": None if quality is None else quality["rmse"],
-            "bit_exact": None if quality is None else quality["bit_exact"],
+            "rmse": quality["rmse"] if quality is not None else (
+                parity["rmse"] if parity is not None else None),
+            "bit_exact": quality["bit_exact"] if quality is not None else (
+                parity["bit_exact"] if parity is not None else None),
             "quality": quality,
             "setup": setup,
             "first_render_ms": round(first_ms, 2) if world == 1 else None,
@@ -673,9 +803,16 @@ def main() -> None:
             line["scaling_anchors"] = anchors
         if one_gpu is not None:
             line["one_gpu_same_workload"] = one_gpu
-            line["speedup_vs_one_gpu_same_workload"] = round(one_gpu["kernel_ms"] / ms_step, 3)
-        if shard_exact is not None:
-            line["shard_exact"] = shard_exact
+            # like for like: kernel time against the max-over-ranks kernel
+            # time of a step, wall time against ms_per_step
+            line["speedup_vs_one_gpu_same_workload"] = {
+                "kernel": round(one_gpu["kernel_ms"] / kernel_ms_max, 3),
+                "wall": round(one_gpu["wall_ms"] / ms_step, 3),
+                "kernel_ms_max_over_ranks": round(kernel_ms_max, 3)}
+        if samples:
+            line["reduced_frame_parity"] = parity if parity is not None else (
+                f"not checked: no committed reduced-frame fixture for {nx}x{ny}, {args.spp} spp, depth "
+                f"{args.depth} at N = {world} (tools/make_golden_reduced.py)")
         if check is not None:
             line["check_reduced_canvas" + ("" if samples else "_equals_single_render")] = check
         beat.stop()

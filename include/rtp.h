@@ -320,7 +320,9 @@ int32_t rtp_sphere_walk(rtp_context* ctx);
 /* Diagnostics: the octant mask of the current scene's global sphere walk (a
  * ray in direction octant o walks the near-to-far copy o & mask; 7: all 8
  * copies, the default for the host SAH and the device LBVH builds alike;
- * RTP_BVH_OCT_MASK narrows it for experiments); -1 without a sphere BVH. */
+ * RTP_BVH_OCT_MASK narrows it for experiments); -1 without a sphere BVH.  The
+ * value is copied back from the device scene the kernels read (-2 if that
+ * copy fails, -3 if it disagrees with the context's host mirror). */
 int32_t rtp_sphere_walk_oct_mask(rtp_context* ctx);
 
 /* Diagnostics: exhaustively compare a fast device arithmetic sequence with the

@@ -86,6 +86,55 @@ def build_cpp(force: bool = False) -> list[str]:
     return built
 
 
+ASAN_DIR = os.path.join(ROOT, "tests", "cpp", "asan")
+# programs linked against the host-sanitized library sources (not librtp.so)
+ASAN_PROGRAMS = {
+    os.path.join(ASAN_DIR, "asan_scene"): os.path.join(ROOT, "tests", "cpp", "asan_scene.cpp"),
+    os.path.join(ASAN_DIR, "shim_check"): os.path.join(ROOT, "tests", "cpp", "shim_check.cpp"),
+}
+# AddressSanitizer + UBSan on host code only (GPU sanitizers are not available
+# on the pool): each -fsanitize= directly after -Xarch_host.  The sanitizer
+# runtime links statically into the executables (clang's default).
+ASAN_HOST = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+             "-Xarch_host", "-fno-omit-frame-pointer", "-Xarch_host", "-fno-sanitize-recover=undefined"]
+
+
+def build_asan(force: bool = False) -> list[str]:
+    """Host-sanitized builds of the library's sources linked into the test
+    drivers of tests/cpp (one object per source, cached by mtime)."""
+    os.makedirs(ASAN_DIR, exist_ok=True)
+    base = [hipcc(), "-O1", "-g", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+            "-fno-slp-vectorize", *ASAN_HOST]
+    hdrs = [os.path.join(CSRC, f) for f in HEADERS]
+    newest_hdr = max(os.path.getmtime(h) for h in hdrs if os.path.exists(h))
+    objs = []
+    for s in SOURCES:
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(ASAN_DIR, s + ".o")
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), newest_hdr):
+            res = subprocess.run([*base, "-fPIC", "-c", src, "-o", obj + ".tmp"], capture_output=True, text=True)
+            if res.returncode != 0:
+                raise RuntimeError(f"hipcc (asan) failed for {s}:\n{res.stderr}")
+            os.replace(obj + ".tmp", obj)
+        objs.append(obj)
+    inc = os.path.join(ROOT, "include")
+    built = []
+    for exe, src in ASAN_PROGRAMS.items():
+        deps = objs + [src, os.path.join(inc, "rtp.h"), os.path.join(inc, "rtp", "rendering.hpp")]
+        if force or not os.path.exists(exe) or any(os.path.getmtime(d) > os.path.getmtime(exe) for d in deps):
+            # the driver is host C++ (g++-style, like build_cpp), the link
+            # pulls in the HIP runtime and the static sanitizer runtimes
+            res = subprocess.run([*base, "-x", "c++", "-I", inc, "-c", src, "-o", exe + ".o"], capture_output=True,
+                                 text=True)
+            if res.returncode == 0:
+                res = subprocess.run([hipcc(), "-fsanitize=address,undefined", exe + ".o", *objs, "-o", exe],
+                                     capture_output=True, text=True)
+            if res.returncode != 0:
+                raise RuntimeError(f"hipcc (asan) build failed for {src}:\n{res.stderr[-4000:]}")
+        built.append(exe)
+    return built
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
     print("\n".join(build_cpp(force="--force" in sys.argv)))

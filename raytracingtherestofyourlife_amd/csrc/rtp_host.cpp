@@ -974,9 +974,9 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
   }
   if (e == hipSuccess) e = hipMemcpy(c->d_scene, h, sizeof(*h), hipMemcpyHostToDevice);
   c->lw_bytes = h->n_lw_nodes > 0 ? 16 * (8 * h->n_lw_nodes + h->n_lw_sph) : 0;
-  delete h;
   c->use_bvh = use_bvh;
-  c->oct_mask = use_bvh ? h->oct_mask : 0;
+  c->oct_mask = use_bvh ? h->oct_mask : 0;  // (read before the host copy is freed)
+  delete h;
   if (e != hipSuccess) return hip_fail(e, "rtp_set_scene upload");
   c->kept_quads = std::move(kept_ref);
   c->n_ref_quads = s->n_quads;
@@ -1372,7 +1372,14 @@ int32_t rtp_sphere_walk(rtp_context* c) {
 
 int32_t rtp_sphere_walk_oct_mask(rtp_context* c) {
   if (!c || !c->has_scene || !c->use_bvh) return -1;
-  return c->oct_mask;
+  // the value the kernels read: DevScene::oct_mask of the device copy (the
+  // host field is a mirror, checked against it)
+  int32_t dm = -1;
+  if (hipSetDevice(c->device) != hipSuccess ||
+      hipMemcpy(&dm, reinterpret_cast<const char*>(c->d_scene) + offsetof(rtp::DevScene, oct_mask), sizeof(dm),
+                hipMemcpyDeviceToHost) != hipSuccess)
+    return -2;
+  return dm == c->oct_mask ? dm : -3;
 }
 
 // Diagnostics: exhaustive device check of a fast arithmetic sequence (kind,

@@ -15,7 +15,9 @@ from _util import assert_render_equal, load_full_frame, rmse_normalized, same_bi
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 FULL_FRAMES = ["c2_full"]  # whole frames (byte-plane format, tools/make_golden.py full_frame_fixture)
 RENDERS = sorted(n for n in (os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLD, "*.npz")))
-                 if n not in FULL_FRAMES and not n.endswith("_digest"))  # (digest fixtures: test_gpu_fullsize)
+                 if n not in FULL_FRAMES and not n.endswith("_digest")  # (digest fixtures: test_gpu_fullsize)
+                 and not n.startswith("c5_reduced"))  # (reduced-frame fixtures: below)
+REDUCED = ["c5_reduced", "c5_reduced_small"]
 
 
 def _load(name):
@@ -218,3 +220,63 @@ def test_c5_band_digest_is_the_full_digests_leading_band():
     assert n == int(full["nx"]) * int(full["ny"]) // 2
     assert np.array_equal(full["nan_pixels"][full["nan_pixels"] < n], band["nan_pixels"])
     assert int(band["live_sum"]) < int(full["live_sum"])
+
+
+def _reduced_cases(g):
+    from raytracingtherestofyourlife_amd.shard import sample_batches
+
+    npix = int(g["nx"]) * int(g["ny"])
+    for n in g["worlds"]:
+        for b in sample_batches(int(g["spp"]), int(n), npix):
+            yield int(n), b
+
+
+@pytest.mark.parametrize("name", REDUCED)
+def test_reduced_fixture_is_its_shards_summed(name):
+    """tools/make_golden_reduced.py: reduced_N is the rank-order float32 sum
+    of shards_N, and the shards' final seeds differ per rank (derived streams)."""
+    g = _load(name)
+    for n in g["worlds"]:
+        sh = g[f"shards_{n}"]
+        acc = sh[0].copy()
+        for x in sh[1:]:
+            acc = acc + x
+        same = (acc.view(np.uint32) == g[f"reduced_{n}"].view(np.uint32)) | (np.isnan(acc) & np.isnan(g[f"reduced_{n}"]))
+        assert same.all()
+        assert len({int(s[0]) for s in g[f"final_seed_{n}"]}) == n
+
+
+@pytest.mark.parametrize("name", REDUCED)
+def test_oracle_reproduces_reduced_fixture(oracle, name):
+    """A few pixels of every rank's shard re-rendered by the oracle."""
+    g = _load(name)
+    nx, ny = int(g["nx"]), int(g["ny"])
+    sc = oracle.cornell_box(int(g["variant"]))
+    cam = oracle.camera_setup(nx, ny)
+    k = 4 if nx * ny > 10**6 else 24
+    for n, b in _reduced_cases(g):
+        if b.rank not in (0, n - 1):
+            continue
+        got = oracle.render_pixels(sc, cam, nx, ny, b.spp, int(g["depth"]), g["pixels"][:k], seed_base=b.seed_base)
+        want = (np.c_[g[f"shards_{n}"][b.rank][:k], np.zeros(k, np.float32)], g[f"final_seed_{n}"][b.rank][:k],
+                g[f"live_{n}"][b.rank][:k])
+        assert_render_equal(got, want, f"{name} N={n} rank {b.rank}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", REDUCED)
+def test_hip_reproduces_reduced_fixture(device, name):
+    """Every rank's shard of every world size, all fixture pixels, bit-exact
+    (C5: 1024 pixels x 16384 spp per N)."""
+    import raytracingtherestofyourlife_amd as rtp
+
+    g = _load(name)
+    device.set_cornell_box(int(g["variant"]))
+    nx, ny = int(g["nx"]), int(g["ny"])
+    m = len(g["pixels"])
+    for n, b in _reduced_cases(g):
+        got = device.render_pixels(rtp.default_camera(), nx, ny, b.spp, int(g["depth"]), g["pixels"],
+                                   seed_base=b.seed_base)[:3]
+        want = (np.c_[g[f"shards_{n}"][b.rank], np.zeros(m, np.float32)], g[f"final_seed_{n}"][b.rank],
+                g[f"live_{n}"][b.rank])
+        assert_render_equal(got, want, f"{name} N={n} rank {b.rank}")

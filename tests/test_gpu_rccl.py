@@ -57,4 +57,7 @@ def test_bench_rccl_sample_shard_path_on_one_rank():
     chk = line["check_reduced_canvas"]
     assert chk["reduced_equals_sum_of_shards_max_rel"] == 0.0 and chk["nan_pattern_equal"]
     assert chk["consistent"] is True
-    assert line["speedup_vs_one_gpu_same_workload"] > 0
+    sp = line["speedup_vs_one_gpu_same_workload"]
+    assert sp["kernel"] > 0 and sp["wall"] > 0
+    # no committed reduced-frame fixture for this N = 1 configuration: said so
+    assert line["reduced_frame_parity"].startswith("not checked")
