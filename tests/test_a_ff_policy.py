@@ -105,3 +105,7 @@ def _wait_for_device_memory(timeout_s: float = 60.0) -> None:
         if free > total - (16 << 30):
             return
         time.sleep(0.5)
+    free, total = torch.cuda.mem_get_info(0)
+    pytest.fail(f"the child's jump tables were not released within {timeout_s:.0f} s: "
+                f"{free / 2**30:.1f} of {total / 2**30:.1f} GiB free (later table builds would fail with an "
+                f"unrelated out-of-memory error)")

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import argparse
 import hashlib
+import json
 import os
 import sys
 import time
@@ -65,6 +66,21 @@ def main() -> None:
     a = ap.parse_args()
     work = os.path.join(a.work, a.name)
     os.makedirs(work, exist_ok=True)
+    # the chunk cache is valid only for the configuration that wrote it: a
+    # manifest records it, and a different one under the same name is refused
+    config = {"variant": a.variant, "nx": a.nx, "ny": a.ny, "spp": a.spp, "depth": a.depth,
+              "seed_base": a.seed_base, "chunks": a.chunks}
+    manifest = os.path.join(work, "manifest.json")
+    if os.path.exists(manifest):
+        with open(manifest) as f:
+            old = json.load(f)
+        if old != config:
+            raise SystemExit(f"{work} holds chunks of another configuration ({old}); remove it or use another --work")
+    else:
+        if any(fn.startswith("chunk") for fn in os.listdir(work)):
+            raise SystemExit(f"{work} holds chunks without a manifest; remove them or use another --work")
+        with open(manifest, "w") as f:
+            json.dump(config, f)
     sc = oc.cornell_box(a.variant)
     cam = oc.camera_setup(a.nx, a.ny)
     n = a.nx * a.ny
@@ -80,7 +96,7 @@ def main() -> None:
         pix = np.arange(bounds[c], bounds[c + 1], dtype=np.int64)
         rgba, seeds, live = oc.render_pixels(sc, cam, a.nx, a.ny, a.spp, a.depth, pix, seed_base=a.seed_base,
                                              nthreads=a.threads)
-        np.savez(f + ".tmp.npz", rgb=rgba[:, :3], seeds=seeds, live=live)
+        np.savez(f + ".tmp.npz", rgb=rgba[:, :3], seeds=seeds, live=live, begin=bounds[c], end=bounds[c + 1])
         os.replace(f + ".tmp.npz", f)
         print(f"chunk {c + 1}/{a.chunks} ({pix.size} px): {time.time() - t0:.0f}s", flush=True)
     k = a.chunks if a.assemble_first is None else a.assemble_first
@@ -88,9 +104,13 @@ def main() -> None:
     if missing:
         raise SystemExit(f"{len(missing)} chunks still missing (first {missing[:4]})")
     parts = [np.load(os.path.join(work, f"chunk{c:04d}.npz")) for c in range(k)]
+    for c, p in enumerate(parts):
+        if (int(p["begin"]), int(p["end"])) != (int(bounds[c]), int(bounds[c + 1])) or len(p["rgb"]) != bounds[c + 1] - bounds[c]:
+            raise SystemExit(f"chunk {c} does not cover pixels [{bounds[c]}, {bounds[c + 1]})")
     rgb = np.concatenate([p["rgb"] for p in parts])
     seeds = np.concatenate([p["seeds"] for p in parts])
     live = np.concatenate([p["live"] for p in parts])
+    assert len(rgb) == len(seeds) == len(live) == bounds[k]
     out = os.path.join(ROOT, "tests", "golden", a.name + ".npz")
     np.savez_compressed(out, variant=a.variant, nx=a.nx, ny=a.ny, spp=a.spp, depth=a.depth, camera=cam,
                         seed_base=a.seed_base, pixel_begin=0, pixel_count=int(bounds[k]),
