@@ -105,10 +105,11 @@ def test_gpu_prefilter_equals_exact_scan(device, variant):
     bad = np.nonzero((got[:, 0:3] != got[:, 3:6]).any(1))[0]
     assert bad.size == 0, f"{bad.size} rays differ, first {rays[bad[:3]].tolist()} -> {got[bad[:3]].tolist()}"
     # the prefilter must actually engage on this scene (axis-plane quads):
-    # column 6 is 0 (prefilter decided), 1 (fell back to the exact scan) or
-    # 2 (prefilter off for the scene)
-    assert (got[:, 6] != 2).all()
-    assert (got[:, 6] == 1).mean() < 0.5
+    # column 6 & 3 is 0 (prefilter decided), 1 (fell back to the exact scan)
+    # or 2 (prefilter off for the scene); bit 4: the box cull fell back
+    assert (got[:, 6] & 3 != 2).all()
+    assert (got[:, 6] & 3 == 1).mean() < 0.5
+    assert device.box_cull()
 
 
 def test_gpu_prefilter_fallback_rate(device):
@@ -120,8 +121,12 @@ def test_gpu_prefilter_fallback_rate(device):
     ordinary = np.concatenate([rays[6 * k:], rays[k:2 * k]])
     got = device.debug_closest_hit(ordinary)
     assert (got[:, 0:3] == got[:, 3:6]).all()
-    assert (got[:, 6] != 2).all()
-    assert (got[:, 6] == 1).mean() < 0.01, (got[:, 6] == 1).mean()
+    assert (got[:, 6] & 3 != 2).all()
+    assert (got[:, 6] & 3 == 1).mean() < 0.01, (got[:, 6] & 3 == 1).mean()
+    # the box cull: camera rays fall back rarely (the other populations here
+    # include origins on the box's faces going into it at random angles)
+    cam = (got[:k, 6] & 4) != 0  # ordinary[:k] = rays[6k:7k]: the camera rays
+    assert cam.mean() < 0.002, cam.mean()
 
 
 def test_gpu_prefilter_bvh_scene_equals_exact(device):
@@ -161,6 +166,141 @@ def test_gpu_prefilter_with_trapezoid_in_axis_plane(device):
         got = device.debug_closest_hit(rays)
         bad = np.nonzero((got[:, 0:3] != got[:, 3:6]).any(1))[0]
         assert bad.size == 0, f"{bad.size} rays differ, first {rays[bad[:3]].tolist()}"
-        assert (got[:, 6] != 2).all(), "prefilter switched off by one non-parallelogram quad"
+        assert (got[:, 6] & 3 != 2).all(), "prefilter switched off by one non-parallelogram quad"
     finally:
         device.set_cornell_box(0)
+
+
+# ---------------------------------------------------------------- box cull --
+# The rotated box of the reference scene (CornellBox.cpp: the tall box, quads
+# 6..11 of the scene, turned -15 degrees about y): four vertical sides
+# between y = 0 and 330/555, the bottom at 0, a cap whose corner
+# (265, 333, 295)/555 is raised 3 units above the sides' top.
+def box_quads(verts):
+    ys = verts[:, :, 1]
+    sides = [q for q in range(len(verts)) if np.unique(ys[q]).size == 2 and ys[q].min() == 0
+             and np.isclose(ys[q].max(), 330 / 555)]
+    cap = [q for q in range(len(verts)) if ys[q].min() > 0.5 and np.isclose(ys[q].min(), 330 / 555)]
+    return sides, cap[0]
+
+
+def box_rays(verts, n, seed):
+    """Rays where the box cull's decisions are closest to wrong: aimed at the
+    box's vertical edges, its top rim, the cap's corners and diagonal and the
+    gap under the raised cap corner (ulp-nudged), from above, the side and
+    inside; leaving its faces; grazing its sides; nearly vertical."""
+    rng = np.random.default_rng(seed)
+    sides, cap = box_quads(verts)
+    C = verts[cap]  # v00 is the raised corner
+    k = n // 8
+    out = []
+
+    def nudge(p, ulps=400):
+        u = rng.integers(-ulps, ulps + 1, p.shape) * (rng.uniform(0, 1, p.shape) < 0.6)
+        return (np.asarray(p, np.float32).view(np.int32) + u.astype(np.int32)).view(np.float32)
+
+    def aimed(o, tgt):
+        return np.concatenate([o, (nudge(tgt) - o).astype(np.float32)], 1)
+
+    # 1. from anywhere in the room at points on the sides' edges (vertical
+    #    edges, top rim at 330, bottom rim) and corners
+    q = rng.choice(sides, k)
+    e = rng.integers(0, 4, k)
+    s = rng.uniform(0, 1, k)
+    s[rng.uniform(0, 1, k) < 0.25] = 0.0
+    a, b = verts[q, e], verts[q, (e + 1) % 4]
+    out.append(aimed(rng.uniform(0.01, 0.99, (k, 3)).astype(np.float32), a + s[:, None] * (b - a)))
+    # 2. from above (ceiling, light) at the cap: corners, edges, its diagonal v10-v01
+    o = np.c_[rng.uniform(0.05, 0.95, k), rng.uniform(0.62, 0.999, k), rng.uniform(0.05, 0.95, k)].astype(np.float32)
+    j = rng.integers(0, 4, k)
+    s = rng.uniform(0, 1, k)
+    s[rng.uniform(0, 1, k) < 0.3] = 0.0
+    diag = rng.uniform(0, 1, k) < 0.3
+    a = np.where(diag[:, None], C[1], C[j])
+    b = np.where(diag[:, None], C[3], C[(j + 1) % 4])
+    out.append(aimed(o, a + s[:, None] * (b - a)))
+    # 3. into the gap under the raised corner: points on the two sides meeting
+    #    at it, between y = 330 and 333 (and just outside the footprint)
+    tgt = C[0][None, :] + rng.uniform(0, 1, (k, 1)) * (C[rng.choice([1, 3], k)] - C[0][None, :])
+    tgt[:, 1] = rng.uniform(329.5, 333.5, k) / 555.0
+    o = rng.uniform(0.01, 0.99, (k, 3)).astype(np.float32)
+    out.append(aimed(o, tgt.astype(np.float32)))
+    # 4. origins inside the box (under the cap), random directions
+    lo, hi = verts[sides].reshape(-1, 3).min(0), verts[sides].reshape(-1, 3).max(0)
+    o = rng.uniform(lo, hi, (k, 3)).astype(np.float32)
+    out.append(np.concatenate([o, rng.normal(size=(k, 3)).astype(np.float32)], 1))
+    # 5. leaving a side or the cap (origins on the face), cosine-like outward
+    #    and grazing directions
+    q = rng.choice(sides + [cap], k)
+    u, v = rng.uniform(0, 1, (2, k))
+    v00, v10, v01 = verts[q, 0], verts[q, 1], verts[q, 3]
+    o = (v00 + u[:, None] * (v10 - v00) + v[:, None] * (v01 - v00)).astype(np.float32)
+    nrm = np.cross(v10 - v00, v01 - v00)
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    t = rng.normal(size=(k, 3))
+    t -= (t * nrm).sum(1, keepdims=True) * nrm
+    h = (10.0 ** rng.uniform(-7, 0, (k, 1))) * np.where(rng.uniform(0, 1, (k, 1)) < 0.5, 1, -1)
+    out.append(np.concatenate([o, (t + h * nrm).astype(np.float32)], 1))
+    # 6. grazing the sides: directions within 1e-7..1e-1 rad of a side's
+    #    plane, passing near it
+    q = rng.choice(sides, k)
+    u, v = rng.uniform(-0.1, 1.1, (2, k))
+    v00, v10, v01 = verts[q, 0], verts[q, 1], verts[q, 3]
+    p = v00 + u[:, None] * (v10 - v00) + v[:, None] * (v01 - v00)
+    nrm = np.cross(v10 - v00, v01 - v00)
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    t = rng.normal(size=(k, 3))
+    t -= (t * nrm).sum(1, keepdims=True) * nrm
+    t /= np.linalg.norm(t, axis=1, keepdims=True)
+    ang = (10.0 ** rng.uniform(-7, -1, (k, 1))) * np.where(rng.uniform(0, 1, (k, 1)) < 0.5, 1, -1)
+    d = t + ang * nrm
+    o = p - rng.uniform(0.05, 0.6, (k, 1)) * d
+    out.append(np.concatenate([o, d], 1).astype(np.float32))
+    # 7. nearly vertical rays over the footprint and its rim (tiny x, z)
+    o = np.c_[rng.uniform(lo[0] - 0.02, hi[0] + 0.02, k), rng.uniform(0.62, 0.99, k),
+              rng.uniform(lo[2] - 0.02, hi[2] + 0.02, k)].astype(np.float32)
+    d = np.c_[rng.normal(size=k) * 10.0 ** rng.uniform(-8, -1, k), -np.ones(k),
+              rng.normal(size=k) * 10.0 ** rng.uniform(-8, -1, k)].astype(np.float32)
+    out.append(np.concatenate([o, d], 1))
+    # 8. the render's populations near the box: camera rays at it, bounces from
+    #    the floor and walls toward random points on it
+    eye = np.array([278, 278, -800], np.float32) / np.float32(555)
+    q = rng.choice(sides + [cap], k)
+    u, v = rng.uniform(0, 1, (2, k))
+    tgt = verts[q, 0] + u[:, None] * (verts[q, 1] - verts[q, 0]) + v[:, None] * (verts[q, 3] - verts[q, 0])
+    half = k // 2
+    o = np.c_[rng.uniform(0, 1, k), np.zeros(k), rng.uniform(0, 1, k)].astype(np.float32)
+    o[:half] = eye
+    out.append(np.concatenate([o, (tgt - o).astype(np.float32)], 1))
+    return np.ascontiguousarray(np.concatenate(out, 0), dtype=np.float32)
+
+
+@pytest.mark.parametrize("variant", [0, 2])
+def test_gpu_box_cull_equals_exact_scan(device, variant):
+    device.set_cornell_box(variant)
+    assert device.box_cull()
+    verts = scene_quads(variant)
+    rays = box_rays(verts, 1 << 21, 200 + variant)
+    got = device.debug_closest_hit(rays)
+    bad = np.nonzero((got[:, 0:3] != got[:, 3:6]).any(1))[0]
+    assert bad.size == 0, f"{bad.size} rays differ, first {rays[bad[:3]].tolist()} -> {got[bad[:3]].tolist()}"
+    k = len(rays) // 8
+    fb = (got[:, 6] & 4) != 0
+    # the hard populations fall back often (by design), the render's rarely
+    assert fb[:5 * k].mean() > 0.01
+    assert fb[7 * k:].mean() < 0.005, fb[7 * k:].mean()
+    device.set_cornell_box(0)
+
+
+def test_gpu_box_cull_off_switch(device, monkeypatch):
+    """RTP_BOXCULL=0 at rtp_set_scene: every quad scanned exactly, same hits."""
+    monkeypatch.setenv("RTP_BOXCULL", "0")
+    device.set_cornell_box(0)
+    assert not device.box_cull()
+    verts = scene_quads(0)
+    rays = box_rays(verts, 1 << 16, 9)
+    got = device.debug_closest_hit(rays)
+    assert (got[:, 0:3] == got[:, 3:6]).all() and ((got[:, 6] & 4) == 0).all()
+    monkeypatch.delenv("RTP_BOXCULL")
+    device.set_cornell_box(0)
+    assert device.box_cull()

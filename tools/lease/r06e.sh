@@ -1,0 +1,8 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_prefilter.py tests/test_golden.py -k "prefilter or box or c2_full or hip_reproduces" > gpurun_out/r06e_tests.txt 2>&1
+rc=$?
+echo "tests rc=$rc" >> gpurun_out/r06e_tests.txt
+if [ $rc -ne 0 ]; then exit $rc; fi
+RTP_DEBUG_STATS=1 timeout -k 10 120 python tools/box_cull_rate.py --spp 16 > gpurun_out/r06e_rates.txt 2>&1 || exit 1
+timeout -k 10 500 tools/ab.sh 3 main build_exp/lib_base.so > gpurun_out/r06e_ab_c2.txt 2>&1
