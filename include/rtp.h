@@ -325,14 +325,6 @@ int32_t rtp_sphere_walk(rtp_context* ctx);
  * copy fails, -3 if it disagrees with the context's host mirror). */
 int32_t rtp_sphere_walk_oct_mask(rtp_context* ctx);
 
-/* Diagnostics: 1 if closest-hit searches of the current scene cull its box
- * rotated about y (four vertical sides and a bottom between two heights, a cap
- * quad over their footprint: the sides' and bottom's exact tests run only for
- * rays the cull cannot decide), 0 if every quad is scanned
- * exactly (other scenes, RTP_BOXCULL=0 at rtp_set_scene, or the prefilter off);
- * read back from the device scene (-1 without a scene, -2 if the copy fails). */
-int32_t rtp_box_cull(rtp_context* ctx);
-
 /* Diagnostics: exhaustively compare a fast device arithmetic sequence with the
  * IEEE operation for every float bit pattern in [lo_bits, hi_bits].  kind 0:
  * rcp (v_rcp + 1 Newton step) vs 1.0f/x; 1: rcp + remainder correction; 2:

@@ -74,7 +74,7 @@ EXPORTED_SYMBOLS = [
     "rtp_eval_primitive", "rtp_debug_counters", "rtp_verify_fast_math", "rtp_debug_closest_hit",
     "rtp_render_direct", "rtp_render_direct_device", "rtp_sample_color_table", "rtp_quad_scalars",
     "rtp_cornell_point_field", "rtp_write_pnm_depth", "rtp_eval_powf", "rtp_set_ff_tables", "rtp_get_ff_tables",
-    "rtp_render_planned_device", "rtp_sphere_walk", "rtp_sphere_walk_oct_mask", "rtp_box_cull",
+    "rtp_render_planned_device", "rtp_sphere_walk", "rtp_sphere_walk_oct_mask",
 ]
 
 
@@ -153,12 +153,8 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.rtp_get_ff_tables.argtypes = [vp, ctypes.POINTER(RtpFfInfo)]
     L.rtp_sphere_walk.argtypes = [vp]
     L.rtp_sphere_walk_oct_mask.argtypes = [vp]
-    if hasattr(L, "rtp_box_cull") or not os.environ.get("RTP_LIB_PATH"):  # (older experiment builds lack it)
-        L.rtp_box_cull.argtypes = [vp]
     for name in EXPORTED_SYMBOLS:
         if name not in ("rtp_last_error", "rtp_abi_version", "rtp_destroy"):
-            if name == "rtp_box_cull" and os.environ.get("RTP_LIB_PATH") and not hasattr(L, name):
-                continue
             getattr(L, name).restype = ctypes.c_int32
     _lib = L
     return L

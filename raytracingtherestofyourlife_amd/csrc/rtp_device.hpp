@@ -334,17 +334,20 @@ RTP_DEV f2v dot_m2l(const float* x, const f2v (&y)[3]) {  // dot_m with a shared
   else return f2v{0.0f, 0.0f};
 }
 
-// The exact-parallelogram form of quad_hit_masked<K> (e21 == -e03, e23 ==
-// -e01 bit for bit), on P = cross(d, e03), det and its reciprocal: also the
-// rotated-box cull's per-lane test of its candidate face (K = 0, the full
-// products on a scan head read from LDS: bit-equal to the face's own kind,
-// see the zero-structure note above).
-template <int K, class G>
-RTP_DEV bool quad_hit_para(const G& Q, f3 o, f3 d, const float (&P)[3], float det, float inv_det, float& t_out) {
-  constexpr int M01 = kQuadKind[K].m01, M03 = kQuadKind[K].m03;
-  constexpr int MP = cross_mask(M03), MQ = cross_mask(M01);
+// G: the quad's scan head (a DevQuad, or a QuadGeom copy already in
+// registers); M: the quad in memory, read only for the second triangle's
+// edges of a quad that is not an exact parallelogram.
+template <int K, class G = DevQuad>
+RTP_DEV bool quad_hit_masked(const G& Q, const DevQuad& M, f3 o, f3 d, float& t_out) {
+  constexpr int M01 = kQuadKind[K].m01, M03 = kQuadKind[K].m03, M21 = kQuadKind[K].m21, M23 = kQuadKind[K].m23;
+  constexpr int MP = cross_mask(M03), MQ = cross_mask(M01), MPp = cross_mask(M21), MQp = cross_mask(M23);
   const float dv[3] = {d.x, d.y, d.z};
-  {
+  const float P[3] = {cross_c<M03, 0>(dv, Q.e03), cross_c<M03, 1>(dv, Q.e03), cross_c<M03, 2>(dv, Q.e03)};
+  const float det = dot_m<M01 & MP>(Q.e01, P);
+  const float inv_det = rcp_det(det);
+  // (a parallelogram has e21 == -e03 and e23 == -e01, so only kinds whose
+  // masks pair up can hold one)
+  if constexpr (M21 == M03 && M23 == M01) if (Q.para) {
     // exact parallelogram (e21 == -e03, e23 == -e01 bit for bit): Pp == -P,
     // detp == det, Qp == -cross(Tp, e01), so the second triangle is the first
     // one's arithmetic on Tp = o - v11 with both results negated (negation
@@ -372,31 +375,6 @@ RTP_DEV bool quad_hit_para(const G& Q, f3 o, f3 d, const float (&P)[3], float de
     t_out = t;
     return ok1 & !(second & bad2);
   }
-}
-template <int K, class G>
-RTP_DEV bool quad_hit_para(const G& Q, f3 o, f3 d, float& t_out) {
-  constexpr int M01 = kQuadKind[K].m01, M03 = kQuadKind[K].m03;
-  constexpr int MP = cross_mask(M03);
-  const float dv[3] = {d.x, d.y, d.z};
-  const float P[3] = {cross_c<M03, 0>(dv, Q.e03), cross_c<M03, 1>(dv, Q.e03), cross_c<M03, 2>(dv, Q.e03)};
-  const float det = dot_m<M01 & MP>(Q.e01, P);
-  return quad_hit_para<K>(Q, o, d, P, det, rcp_det(det), t_out);
-}
-
-// G: the quad's scan head (a DevQuad, or a QuadGeom copy already in
-// registers); M: the quad in memory, read only for the second triangle's
-// edges of a quad that is not an exact parallelogram.
-template <int K, class G = DevQuad>
-RTP_DEV bool quad_hit_masked(const G& Q, const DevQuad& M, f3 o, f3 d, float& t_out) {
-  constexpr int M01 = kQuadKind[K].m01, M03 = kQuadKind[K].m03, M21 = kQuadKind[K].m21, M23 = kQuadKind[K].m23;
-  constexpr int MP = cross_mask(M03), MQ = cross_mask(M01), MPp = cross_mask(M21), MQp = cross_mask(M23);
-  const float dv[3] = {d.x, d.y, d.z};
-  const float P[3] = {cross_c<M03, 0>(dv, Q.e03), cross_c<M03, 1>(dv, Q.e03), cross_c<M03, 2>(dv, Q.e03)};
-  const float det = dot_m<M01 & MP>(Q.e01, P);
-  const float inv_det = rcp_det(det);
-  // (a parallelogram has e21 == -e03 and e23 == -e01, so only kinds whose
-  // masks pair up can hold one)
-  if constexpr (M21 == M03 && M23 == M01) if (Q.para) return quad_hit_para<K>(Q, o, d, P, det, inv_det, t_out);
   const float T[3] = {o.x - Q.vv[0][0], o.y - Q.vv[1][0], o.z - Q.vv[2][0]};
   const float alpha = dot_m<MP>(T, P) * inv_det;
   const float Qv[3] = {cross_c<M01, 0>(T, Q.e01), cross_c<M01, 1>(T, Q.e01), cross_c<M01, 2>(T, Q.e01)};

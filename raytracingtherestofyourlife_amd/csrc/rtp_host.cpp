@@ -203,203 +203,6 @@ void setup_prefilter(rtp::DevScene* h, const rtp_scene_desc* s, const std::vecto
   h->n_pre = n;
 }
 
-// The rotated-box cull (rtp_layout.hpp BoxCull, rtp_kernels.hip box_cull):
-// enabled when the quads of kinds 7, 8 and 9 are exactly one box turned about
-// y -- four vertical exact parallelograms between two heights whose footprint
-// edges close into a parallelogram (two slabs), and a kind-9 bottom at the
-// lower height over the same four corners -- with one cap quad (kind 10 or 0,
-// scanned exactly) over the footprint at or above the upper height.  Every
-// check is exact or in double with the tolerance below; any miss leaves the
-// cull off (the exact scan of every quad, as before).
-void setup_boxcull(rtp::DevScene* h, const rtp_scene_desc* s, const std::vector<int>& kept) {
-  rtp::BoxCull B;
-  std::memset(&B, 0, sizeof(B));
-  h->box = B;
-  if (h->n_pre <= 0) return;  // (the cull runs where the prefilter does)
-  const char* e = getenv("RTP_BOXCULL");
-  if (e && e[0] == '0') return;
-  const int g7 = h->kind_begin[6], g9 = h->kind_begin[8], g10 = h->kind_begin[9], g11 = h->kind_begin[11];
-  if (g9 - g7 != 4 || h->kind_begin[9] - g9 != 1) return;
-  struct P2 {
-    double x, z;
-    bool operator==(const P2& o) const { return x == o.x && z == o.z; }
-  };
-  auto vert = [&](int pos, int k) {
-    const int32_t* id = s->quad_points + 4 * kept[h->quads[pos].orig];
-    return s->points + 3 * id[k];
-  };
-  float ylo = 0, yhi = 0, scale = 0;
-  P2 seg[4][2];
-  for (int i = 0; i < 4; i++) {
-    const int pos = g7 + i;
-    if (!h->quads[pos].para) return;
-    const float* v[4] = {vert(pos, 0), vert(pos, 1), vert(pos, 2), vert(pos, 3)};
-    float ys[2] = {v[0][1], v[0][1]};
-    for (int k = 0; k < 4; k++) {
-      for (int j = 0; j < 3; j++) {
-        if (!std::isfinite(v[k][j])) return;
-        scale = std::max(scale, std::fabs(v[k][j]));
-      }
-      ys[0] = std::min(ys[0], v[k][1]), ys[1] = std::max(ys[1], v[k][1]);
-    }
-    if (i == 0) ylo = ys[0], yhi = ys[1];
-    if (ys[0] != ylo || ys[1] != yhi || !(ylo < yhi)) return;
-    // two vertices at each height, the upper ones straight above the lower ones
-    int lo[2], n_lo = 0, hi[2], n_hi = 0;
-    for (int k = 0; k < 4; k++) {
-      if (v[k][1] == ylo) {
-        if (n_lo == 2) return;
-        lo[n_lo++] = k;
-      } else if (v[k][1] == yhi) {
-        if (n_hi == 2) return;
-        hi[n_hi++] = k;
-      } else {
-        return;
-      }
-    }
-    if (n_lo != 2 || n_hi != 2) return;
-    for (int a = 0; a < 2; a++) {
-      bool above = false;
-      for (int b = 0; b < 2; b++) above |= v[lo[a]][0] == v[hi[b]][0] && v[lo[a]][2] == v[hi[b]][2];
-      if (!above) return;
-      seg[i][a] = {v[lo[a]][0], v[lo[a]][2]};
-    }
-    if (seg[i][0] == seg[i][1]) return;
-  }
-  // the four segments close into a cycle: every endpoint shared by exactly two
-  std::vector<P2> corners;
-  for (int i = 0; i < 4; i++)
-    for (int a = 0; a < 2; a++) {
-      int n = 0;
-      for (int j = 0; j < 4; j++) n += (seg[j][0] == seg[i][a]) + (seg[j][1] == seg[i][a]);
-      if (n != 2) return;
-      bool seen = false;
-      for (const P2& c : corners) seen |= c == seg[i][a];
-      if (!seen) corners.push_back(seg[i][a]);
-    }
-  if (corners.size() != 4) return;
-  auto shares = [&](int i, int j) {
-    return seg[i][0] == seg[j][0] || seg[i][0] == seg[j][1] || seg[i][1] == seg[j][0] || seg[i][1] == seg[j][1];
-  };
-  int opp1 = -1;
-  for (int j = 1; j < 4; j++)
-    if (!shares(0, j)) opp1 = j;
-  if (opp1 < 0) return;
-  int other[2], no = 0;
-  for (int j = 1; j < 4; j++)
-    if (j != opp1) other[no++] = j;
-  if (no != 2 || shares(other[0], other[1])) return;
-  const double tol = std::ldexp(std::max(1.0, (double)scale), -21);
-  // a slab from a pair of opposite sides: unit normal of the first, both
-  // faces' offsets; slot 2*k is the face at the lower offset (outward -n)
-  auto slab = [&](int a, int c, float* nout, float* cout, int32_t* slots) {
-    const double dx = seg[a][1].x - seg[a][0].x, dz = seg[a][1].z - seg[a][0].z, len = std::hypot(dx, dz);
-    const double nx = -dz / len, nz = dx / len;
-    const double ex = seg[c][1].x - seg[c][0].x, ez = seg[c][1].z - seg[c][0].z;
-    if (std::fabs(dx * ez - dz * ex) > 1e-6 * len * std::hypot(ex, ez)) return false;  // parallel sides
-    double off[2];
-    const int f[2] = {a, c};
-    for (int k = 0; k < 2; k++) {
-      const double p = nx * seg[f[k]][0].x + nz * seg[f[k]][0].z, q = nx * seg[f[k]][1].x + nz * seg[f[k]][1].z;
-      if (std::fabs(p - q) > tol) return false;
-      off[k] = 0.5 * (p + q);
-    }
-    if (!(std::fabs(off[0] - off[1]) > 64 * tol)) return false;
-    const int lo_k = off[0] < off[1] ? 0 : 1;
-    nout[0] = (float)nx, nout[1] = (float)nz;
-    cout[0] = (float)off[lo_k], cout[1] = (float)off[1 - lo_k];
-    slots[0] = g7 + f[lo_k], slots[1] = g7 + f[1 - lo_k];
-    // the float normal and offsets still put every corner on its lines
-    for (const P2& cpt : corners) {
-      const double t = (double)nout[0] * cpt.x + (double)nout[1] * cpt.z;
-      if (std::fabs(t - cout[0]) > tol && std::fabs(t - cout[1]) > tol) return false;
-    }
-    return true;
-  };
-  if (!slab(0, opp1, B.nu, B.cu, B.slot_pos) || !slab(other[0], other[1], B.nv, B.cv, B.slot_pos + 2)) return;
-  auto is_corner_set = [&](int pos, bool* ok_y, float y_eq) {
-    for (int k = 0; k < 4; k++) {
-      const float* v = vert(pos, k);
-      bool in = false;
-      for (const P2& c : corners) in |= c == P2{v[0], v[2]};
-      if (!in) return false;
-      for (int j = 0; j < k; j++)
-        if (vert(pos, j)[0] == v[0] && vert(pos, j)[2] == v[2]) return false;
-      if (ok_y && !(v[1] == y_eq)) *ok_y = false;
-    }
-    return true;
-  };
-  bool flat = true;
-  if (!is_corner_set(g9, &flat, ylo) || !flat) return;  // the bottom
-  // the cap: one quad of the exactly scanned groups over the same corners, at
-  // or above yhi; its triangle planes (Lagae-Dutre: t from (v00, v10, v01),
-  // the second test in (v11, v01, v10)) give the height band over the footprint
-  int cap = -1;
-  for (int pos = g10; pos < g11; pos++) {
-    if (!is_corner_set(pos, nullptr, 0)) continue;
-    if (cap >= 0) return;
-    cap = pos;
-  }
-  if (cap < 0) return;
-  double band_lo = yhi, band_hi = yhi, slope = 0;
-  {
-    double v[4][3];
-    for (int k = 0; k < 4; k++)
-      for (int j = 0; j < 3; j++) v[k][j] = vert(cap, k)[j];
-    for (int k = 0; k < 4; k++)
-      if (!(v[k][1] >= yhi)) return;
-    // the projection is a convex quadrilateral in vertex order
-    double turn0 = 0;
-    for (int k = 0; k < 4; k++) {
-      const double* a = v[k];
-      const double* b = v[(k + 1) % 4];
-      const double* c = v[(k + 2) % 4];
-      const double tn = (b[0] - a[0]) * (c[2] - b[2]) - (b[2] - a[2]) * (c[0] - b[0]);
-      if (k == 0) turn0 = tn;
-      if (!(tn * turn0 > 0)) return;
-    }
-    const int tri[2][3] = {{0, 1, 3}, {2, 3, 1}};
-    for (const auto& T : tri) {
-      const double* p = v[T[0]];
-      const double ux = v[T[1]][0] - p[0], uy = v[T[1]][1] - p[1], uz = v[T[1]][2] - p[2];
-      const double wx = v[T[2]][0] - p[0], wy = v[T[2]][1] - p[1], wz = v[T[2]][2] - p[2];
-      const double n[3] = {uy * wz - uz * wy, uz * wx - ux * wz, ux * wy - uy * wx};
-      if (!(std::fabs(n[1]) > 0.5 * std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]))) return;
-      slope = std::max(slope, (std::fabs(n[0]) + std::fabs(n[2])) / std::fabs(n[1]));
-      for (const P2& c : corners) {
-        const double y = p[1] - (n[0] * (c.x - p[0]) + n[2] * (c.z - p[2])) / n[1];
-        band_lo = std::min(band_lo, y), band_hi = std::max(band_hi, y);
-      }
-    }
-    for (int k = 0; k < 4; k++) band_hi = std::max(band_hi, v[k][1]);
-  }
-  // outward rounding keeps the band conservative
-  B.ylo = ylo, B.yhi = yhi;
-  B.band_lo = std::nextafter(std::nextafter((float)band_lo, -INFINITY), -INFINITY);
-  B.band_hi = std::nextafter(std::nextafter((float)band_hi, INFINITY), INFINITY);
-  // |d.y| >= steep (|d.x| + |d.z|) keeps the ray at least ~4x steeper than
-  // the cap's triangle planes (their determinants far from 0)
-  B.steep = (float)std::max(4.0 * slope, 1.0 / 64);
-  {  // |det| bounds (kEps = vtkm::Epsilon<float>() = 1e-5, rtp_device.hpp)
-    double wmin = INFINITY;
-    for (int i = 0; i < 4; i++) wmin = std::min(wmin, std::hypot(seg[i][1].x - seg[i][0].x, seg[i][1].z - seg[i][0].z));
-    B.sd_min = (float)(2 * 1e-5 / ((double)yhi - ylo) / wmin);
-    double v[4][3];
-    for (int k = 0; k < 4; k++)
-      for (int j = 0; j < 3; j++) v[k][j] = vert(cap, k)[j];
-    auto crs = [](const double* a0, const double* a1, const double* b0, const double* b1, float* out) {
-      const double a[3] = {a1[0] - a0[0], a1[1] - a0[1], a1[2] - a0[2]}, b[3] = {b1[0] - b0[0], b1[1] - b0[1], b1[2] - b0[2]};
-      out[0] = (float)(a[1] * b[2] - a[2] * b[1]), out[1] = (float)(a[2] * b[0] - a[0] * b[2]),
-      out[2] = (float)(a[0] * b[1] - a[1] * b[0]);
-    };
-    crs(v[0], v[1], v[0], v[3], B.cap_n1);  // e01 x e03
-    crs(v[2], v[3], v[2], v[1], B.cap_n2);  // e23 x e21
-  }
-  B.scale = scale;
-  B.on = 1;
-  h->box = B;
-}
-
 // RNG jump tables.  A dead depth consumes 1 + {2,3,2} draws chosen by the
 // `which` draw against two constant thresholds (lightables = 2,
 // MapperPathTracer.cxx:218; PdfWorklet.h:20), so "advance the state over k
@@ -916,9 +719,6 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     }
   }
   setup_prefilter(h, s, kept);
-  setup_boxcull(h, s, kept);
-  if (const char* v = getenv("RTP_VERBOSE"))
-    if (v[0] == '1') fprintf(stderr, "rtp: rotated-box cull %s\n", h->box.on ? "on" : "off");
   h->n_quads = (int32_t)kept.size();
   // the -direct mode's inputs: kept quad -> reference index, and the shape
   // bounds (union of the quads' padded AABBs, AABBSurface.h:36-78)
@@ -1580,16 +1380,6 @@ int32_t rtp_sphere_walk_oct_mask(rtp_context* c) {
                 hipMemcpyDeviceToHost) != hipSuccess)
     return -2;
   return dm == c->oct_mask ? dm : -3;
-}
-
-int32_t rtp_box_cull(rtp_context* c) {
-  if (!c || !c->has_scene) return -1;
-  int32_t on = -1;
-  if (hipSetDevice(c->device) != hipSuccess ||
-      hipMemcpy(&on, reinterpret_cast<const char*>(c->d_scene) + offsetof(rtp::DevScene, box) +
-                         offsetof(rtp::BoxCull, on), sizeof(on), hipMemcpyDeviceToHost) != hipSuccess)
-    return -2;
-  return on;
 }
 
 // Diagnostics: exhaustive device check of a fast arithmetic sequence (kind,

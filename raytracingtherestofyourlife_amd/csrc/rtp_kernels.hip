@@ -294,11 +294,7 @@ constexpr int kLdsQuads = kMaxQuads, kQShadeFloats = 8;  // per quad: n, alb, mt
 // 4 global loads (L2 hits) on every bounce's critical path (C2 kernel -1.7%,
 // r03c; an LDS copy of the quads in round 1 had been slower).
 constexpr int kPrexLdsOffset = kLdsQuads * kQShadeFloats;
-// ... and the rotated-box cull's four side heads (QuadGeom, 64 B each, slot
-// order of BoxCull::slot_pos): the per-lane candidate test reads its face
-// from here (closest_hit)
-constexpr int kBoxLdsOffset = kPrexLdsOffset + kMaxPre * 16;
-constexpr int kQTableFloats = kBoxLdsOffset + 4 * 16;
+constexpr int kQTableFloats = kPrexLdsOffset + kMaxPre * 16;
 
 RTP_DEV void fill_qshade(const DevScene* __restrict__ sc, float* s_qshade) {
   for (int i = threadIdx.x; i < sc->n_quads * kQShadeFloats; i += blockDim.x) {
@@ -308,9 +304,6 @@ RTP_DEV void fill_qshade(const DevScene* __restrict__ sc, float* s_qshade) {
   }
   const float* px = reinterpret_cast<const float*>(sc->prex);
   for (int i = threadIdx.x; i < sc->n_pre * 16; i += blockDim.x) s_qshade[kPrexLdsOffset + i] = px[i];
-  if (sc->box.on)
-    for (int i = threadIdx.x; i < 4 * 16; i += blockDim.x)
-      s_qshade[kBoxLdsOffset + i] = reinterpret_cast<const float*>(sc->quads + sc->box.slot_pos[i >> 4])[i & 15];
 }
 
 // Closest-hit prefilter over the axis-plane quads (kinds 1..6).
@@ -436,105 +429,6 @@ RTP_DEV bool quad_hit_axis(const PreExact& E, f3 o, f3 d, float& t_out) {
   return ok1 & !(second & bad2);
 }
 
-// The rotated-box cull (rtp_layout.hpp BoxCull).  Its four
-// sides and bottom bound a convex prism P (the footprint parallelogram of two
-// slabs u, v times [ylo, yhi]); the cap over it stays in the exact scan.  A
-// lane computes, per slab, the parameters where the ray crosses its two
-// planes (near n <= far f) and for each a margin bounding the difference
-// between that approximation -- and the model plane -- and what the exact
-// Lagae-Dutre test of a face in the plane computes:
-//   w = 2^-18 (max|d| |t| + max|o| + scale + 1) / |n . d|,
-// in t units: 2^-18 of the coordinates along the plane's normal (the
-// prefilter's margin), scaled by the ray's grazing factor.  A face's exact
-// test can accept a hit only at a parameter inside every slab's widened
-// [n - wn, f + wf], and surely accepts one inside the others' narrowed
-// [n + wn, f - wf].  So, every comparison strict and made with the margins:
-//   * the widened intervals have no common point, or they all end before
-//     0.001: no side and no bottom hit is accepted (-1); or they start
-//     after t_best, the hit already found (the cap's and the general quads'
-//     exact scan runs first): every face of P would lose to it (-1);
-//   * the latest near crossing belongs to slab u or v, precedes every far
-//     crossing and follows 0.001: the ray enters P through that side, whose
-//     exact test accepts (if its |det| clears kEps: the tests' det scales
-//     with |d|), and every other face of P is crossed later or outside its
-//     face: the candidate side (its LDS slot 0..3);
-//   * every near crossing is before 0.001 (an origin on a face, going in, or
-//     inside P) and the earliest far crossing belongs to slab u or v, after
-//     0.001: the ray leaves P through that side, the only face it can hit
-//     (the candidate); or it leaves through the open top (no face of P);
-//   * the ray comes down (steeply, so the cap's triangle planes are crossed
-//     far from parallel) into the footprint above the cap's height band
-//     [band_lo, band_hi] and is still inside it below the band and above the
-//     bottom: the cap's exact test accepts a hit in the band (triangle 1's
-//     plane gives t; its v00 wedge and triangle 2's v11 wedge both contain the
-//     footprint) before any face of P: -1;
-//   * anything else -- the gap between the sides' top and a raised cap
-//     corner, near an edge, grazing, degenerate: -2, the exact scan of the
-//     five faces (the caller's fallback).
-#ifndef RTP_BOXCULL_SLIM
-#define RTP_BOXCULL_SLIM 0  // experiment: only the miss, t_best and side-entry cases
-#endif
-struct BoxSlab {
-  float n, f, wn, wf, r;
-};
-RTP_DEV BoxSlab box_slab(float so, float sd, float c0, float c1, float kA, float kB) {
-  BoxSlab S;
-  S.r = __builtin_amdgcn_rcpf(sd);
-  const float a = (c0 - so) * S.r, b = (c1 - so) * S.r;
-  S.n = fminf(a, b);
-  S.f = fmaxf(a, b);
-  const float ar = fabsf(S.r);
-  S.wn = __builtin_fmaf(kA, fabsf(S.n), kB) * ar;
-  S.wf = __builtin_fmaf(kA, fabsf(S.f), kB) * ar;
-  return S;
-}
-RTP_DEV int box_cull(const BoxCull& B, f3 o, f3 d, float omax, float dmax, float t_best) {
-  const float kA = 0x1p-18f * dmax, kB = 0x1p-18f * (omax + B.scale + 1.0f);
-  const float sdu = __builtin_fmaf(B.nu[0], d.x, B.nu[1] * d.z), sdv = __builtin_fmaf(B.nv[0], d.x, B.nv[1] * d.z);
-  const BoxSlab U = box_slab(__builtin_fmaf(B.nu[0], o.x, B.nu[1] * o.z), sdu, B.cu[0], B.cu[1], kA, kB);
-  const BoxSlab V = box_slab(__builtin_fmaf(B.nv[0], o.x, B.nv[1] * o.z), sdv, B.cv[0], B.cv[1], kA, kB);
-  const BoxSlab Y = box_slab(o.y, d.y, B.ylo, B.yhi, kA, kB);
-  // (a degenerate slab -- n . d == 0: r = inf, margins inf -- adds -inf /
-  // +inf / NaN terms that fmaxf / fminf skip: the other slabs alone still
-  // decide a miss; the positive cases below need every slab non-degenerate)
-  const float lo_max = fmaxf(fmaxf(U.n - U.wn, V.n - V.wn), Y.n - Y.wn);
-  const float hi_min = fminf(fminf(U.f + U.wf, V.f + V.wf), Y.f + Y.wf);
-  if (lo_max > hi_min || hi_min < 0.001f || lo_max > t_best) return -1;
-  const float g = 0x1p-20f * dmax;
-  const bool nd = (fabsf(sdu) > g) & (fabsf(sdv) > g) & (fabsf(d.y) > g);
-  // entering P through a side
-  const float ex = fminf(fminf(U.f - U.wf, V.f - V.wf), Y.f - Y.wf);
-  const bool uf = (U.n > V.n) & (U.n > Y.n), vf = (V.n > U.n) & (V.n > Y.n);
-  const float tin = uf ? U.n : V.n, win = uf ? U.wn : V.wn;
-  const float oth = uf ? fmaxf(V.n + V.wn, Y.n + Y.wn) : fmaxf(U.n + U.wn, Y.n + Y.wn);
-  const float sdmin = B.sd_min;
-  if (nd & (uf | vf) & (tin - win > oth) & (tin + win < ex) & (tin - win > 0.001f) &
-      (fabsf(uf ? sdu : sdv) >= sdmin))
-    return uf ? (U.r > 0.0f ? 0 : 1) : (V.r > 0.0f ? 2 : 3);
-#if RTP_BOXCULL_SLIM
-  return -2;
-#endif
-  // every entry behind 0.001: leaving P through a side or the open top
-  const float ent_hi = fmaxf(fmaxf(U.n + U.wn, V.n + V.wn), Y.n + Y.wn);
-  const bool uo = (U.f < V.f) & (U.f < Y.f), vo = (V.f < U.f) & (V.f < Y.f), yo = (Y.f < U.f) & (Y.f < V.f);
-  const float tout = uo ? U.f : vo ? V.f : Y.f, wout = uo ? U.wf : vo ? V.wf : Y.wf;
-  const float oth_f = uo ? fminf(V.f - V.wf, Y.f - Y.wf) : vo ? fminf(U.f - U.wf, Y.f - Y.wf) : fminf(U.f - U.wf, V.f - V.wf);
-  if (nd & (ent_hi < 0.001f) & (uo | vo | (yo & (d.y > 0.0f))) & (tout + wout < oth_f) & (tout - wout > 0.001f) &
-      (yo | (fabsf(uo ? sdu : sdv) >= sdmin)))
-    return uo ? (U.r > 0.0f ? 1 : 0) : vo ? (V.r > 0.0f ? 3 : 2) : -1;
-  // down onto the cap
-  const float bh = (B.band_hi - o.y) * Y.r, bl = (B.band_lo - o.y) * Y.r;
-  const float ay = fabsf(Y.r);
-  const float wbh = __builtin_fmaf(kA, fabsf(bh), kB) * ay, wbl = __builtin_fmaf(kA, fabsf(bl), kB) * ay;
-  const bool steep = fabsf(d.y) >= B.steep * (fabsf(d.x) + fabsf(d.z));
-  const float det1 = __builtin_fmaf(B.cap_n1[0], d.x, __builtin_fmaf(B.cap_n1[1], d.y, B.cap_n1[2] * d.z));
-  const float det2 = __builtin_fmaf(B.cap_n2[0], d.x, __builtin_fmaf(B.cap_n2[1], d.y, B.cap_n2[2] * d.z));
-  const bool dets = (fabsf(det1) >= 2.0f * kEps) & (fabsf(det2) >= 2.0f * kEps);
-  if (nd & steep & dets & (d.y < 0.0f) & (bh - wbh > fmaxf(U.n + U.wn, V.n + V.wn)) & (bh - wbh > 0.001f) & (bl + wbl < ex))
-    return -1;
-  return -2;
-}
-
 // kSpheres = false: the quads only (the pool kernel's resumable sphere-BVH
 // walk, spheres_bvh_step, continues from the quads' hit).
 template <bool kBvh, bool kSpheres = true>
@@ -546,56 +440,22 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
   uint64_t key = kNoHitKey;
   bool full = true;  // this lane needs the exact scan of the axis-plane quads (kinds 1..6)
   const bool pre = prefilter && sc->n_pre > 0;  // wave-uniform
-  const bool cull = pre && sc->box.on;            // wave-uniform
-  bool amb = false;  // (cull) this lane needs the exact scan of the box's five faces
-  // (finite o, d within the margins' range: the prefilter's and the box
-  // cull's approximations hold, and the generic arithmetic equals the kinds')
-  const bool lane_ok = (int)(fabsf(o.x) <= kPreLimD) & (int)(fabsf(o.y) <= kPreLimD) &
-                       (int)(fabsf(o.z) <= kPreLimD) & (int)(fabsf(d.x) <= kPreLimD) &
-                       (int)(fabsf(d.y) <= kPreLimD) & (int)(fabsf(d.z) <= kPreLimD);
-  const float dmax = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fmaxf(fabsf(d.z), 1.0f));
-  const float omax = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
-  {  // kinds 7..10 and 0: the exact scan, always (their keys are final) -- or
-     // with the box cull, kinds 10 and 0, then the cull (kinds 7..9)
+  {  // kinds 7..10 and 0: the exact scan, always (their keys are final)
     const int g6 = sc->kind_begin[6], g7 = sc->kind_begin[7], g8 = sc->kind_begin[8], g9 = sc->kind_begin[9],
               g10 = sc->kind_begin[10], g11 = sc->kind_begin[11];
-    if (!cull) {
-      u16v cur = quad_head(sc, g6);
-      scan_kind_pf<7>(sc, g6, g7, o, d, key, cur);
-      scan_kind_pf<8>(sc, g7, g8, o, d, key, cur);
-      scan_kind_pf<9>(sc, g8, g9, o, d, key, cur);
-      scan_kind_pf<10>(sc, g9, g10, o, d, key, cur);
-      scan_kind_pf<0>(sc, g10, g11, o, d, key, cur);
-    } else {
-      u16v cur = quad_head(sc, g9);
-      scan_kind_pf<10>(sc, g9, g10, o, d, key, cur);
-      scan_kind_pf<0>(sc, g10, g11, o, d, key, cur);
-      const int c = lane_ok ? box_cull(sc->box, o, d, omax, dmax, __uint_as_float((uint32_t)(key >> 32))) : -2;
-      // the candidate side's scan head from the block's LDS table: four
-      // 16-byte reads issued together (c < 0 reads slot 3, unused)
-      const f4v* bx = reinterpret_cast<const f4v*>(lds_prex + (kBoxLdsOffset - kPrexLdsOffset)) + 4 * (c & 3);
-      f4v hr[4] = {bx[0], bx[1], bx[2], bx[3]};
-      static_assert(sizeof(QuadGeom) == sizeof(hr), "a side's scan head is four 16-byte loads");
-      if (c >= 0) {  // (full products on the side's head: bit-equal to its kind 7 / 8 test)
-        QuadGeom G;
-        __builtin_memcpy(&G, hr, sizeof(G));
-        float t;
-        const bool ok = quad_hit_para<0>(G, o, d, t);
-        const uint64_t kq = (uint64_t)__float_as_uint(t) << 32 | G.key_lo;
-        key = (ok && t > 0.001f && kq < key) ? kq : key;
-      }
-      amb = c == -2;
-      if (__ballot(amb)) {
-        if (amb) {
-          cur = quad_head(sc, g6);
-          scan_kind_pf<7>(sc, g6, g7, o, d, key, cur);
-          scan_kind_pf<8>(sc, g7, g8, o, d, key, cur);
-          scan_kind_pf<9>(sc, g8, g9, o, d, key, cur);
-        }
-      }
-    }
+    u16v cur = quad_head(sc, g6);
+    scan_kind_pf<7>(sc, g6, g7, o, d, key, cur);
+    scan_kind_pf<8>(sc, g7, g8, o, d, key, cur);
+    scan_kind_pf<9>(sc, g8, g9, o, d, key, cur);
+    scan_kind_pf<10>(sc, g9, g10, o, d, key, cur);
+    scan_kind_pf<0>(sc, g10, g11, o, d, key, cur);
   }
   if (pre) {
+    const bool lane_ok = (int)(fabsf(o.x) <= kPreLimD) & (int)(fabsf(o.y) <= kPreLimD) &
+                         (int)(fabsf(o.z) <= kPreLimD) & (int)(fabsf(d.x) <= kPreLimD) &
+                         (int)(fabsf(d.y) <= kPreLimD) & (int)(fabsf(d.z) <= kPreLimD);
+    const float dmax = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fmaxf(fabsf(d.z), 1.0f));
+    const float omax = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
     const float ma = kPreK * dmax, mb = kPreK * (omax + (sc->pre_scale + 1.0f));
     uint32_t k1 = ~0u, k2 = ~0u;
     const int p0 = sc->pre_begin[0], p1 = sc->pre_begin[1], p2 = sc->pre_begin[2], p3 = sc->pre_begin[3];
@@ -620,8 +480,7 @@ RTP_DEV Hit closest_hit(const DevScene* __restrict__ sc, f3 o, f3 d, bool prefil
     }
     full = !lane_ok || (k2 & ~31u) <= (uint32_t)(key >> 32);  // k2 = ~0u (none) never is
   }
-  // 2: prefilter off for this scene; + 4: the box cull fell back to its exact scan
-  if (full_out) *full_out = (!pre ? 2u : full ? 1u : 0u) | (amb ? 4u : 0u);
+  if (full_out) *full_out = !pre ? 2u : full ? 1u : 0u;  // 2: prefilter off for this scene
   if (__ballot(full)) {
     if (full) {
       const int g0 = sc->kind_begin[0], g1 = sc->kind_begin[1], g2 = sc->kind_begin[2], g3 = sc->kind_begin[3],
@@ -724,12 +583,9 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
   uint32_t fb = 0;  // (stats) 1: this lane ran the exact scan of the prefiltered quads
   Hit h = closest_hit<kBvh>(sc, org, dir, true, st ? &fb : nullptr, qshade + kPrexLdsOffset);
   if (st) {
-    const unsigned long long m = __ballot((fb & 3u) == 1u);
+    const unsigned long long m = __ballot(fb == 1u);
     dbg[kDbgFallbackSteps] += m ? 1 : 0;
     dbg[kDbgFallbackLanes] += (unsigned long long)__popcll(m);
-    const unsigned long long mb = __ballot((fb & 4u) != 0u);
-    dbg[kDbgBoxFbSteps] += mb ? 1 : 0;
-    dbg[kDbgBoxFbLanes] += (unsigned long long)__popcll(mb);
   }
   if (st) {
     const unsigned long long t1s = __builtin_amdgcn_s_memtime();

@@ -181,31 +181,6 @@ struct alignas(16) PreExact {
   int32_t pad[3];
 };
 
-// Closest-hit cull of a box rotated about y (rtp_kernels.hip
-// box_cull): four vertical exact-parallelogram sides (kinds 7, 8) whose
-// footprint is the parallelogram of two slabs, a bottom face (kind 9) at the
-// sides' lower height, and a cap quad over the footprint (scanned exactly).
-// The model planes lie within 2^-21 (max |coordinate|, 1) of the float faces
-// (rtp_host.cpp setup_boxcull checks).  The sides' scan heads sit in the
-// block's LDS table in slot order [u lo, u hi, v lo, v hi].
-struct alignas(16) BoxCull {
-  int32_t on;             // 1: the sides and the bottom are culled (groups kinds 7, 8, 9 = exactly these 5)
-  int32_t slot_pos[4];    // quads[] position of the side in LDS slot 0..3
-  float nu[2], nv[2];     // unit normals (x, z) of the two side slabs
-  float cu[2], cv[2];     // slab offsets lo < hi: n . p of the two faces of a slab
-  float ylo, yhi;         // the sides' heights (the bottom face lies at ylo)
-  float band_lo, band_hi; // the cap's triangle planes' heights over the footprint, with yhi
-  float steep;            // the cap case needs |d.y| >= steep * (|d.x| + |d.z|)
-  float scale;            // max |coordinate| of the box's vertices
-  // the exact tests reject |det| < kEps: a side's det is +-(its height x
-  // its width) (n . d), the cap's triangles' dets are d . (e01 x e03) and
-  // d . (e23 x e21); a claimed hit needs them clear of kEps
-  float sd_min;           // 2 kEps / (height x the narrowest side's width)
-  float cap_n1[3], cap_n2[3];
-  int32_t pad[2];
-};
-static_assert(sizeof(BoxCull) == 112, "BoxCull: seven 16-byte rows");
-
 struct alignas(16) DevScene {
   int32_t n_quads;
   int32_t n_spheres;
@@ -249,7 +224,6 @@ struct alignas(16) DevScene {
   // (fewer distinct copies: a smaller footprint in the texture cache)
   int32_t oct_mask;
   int32_t pad3[2];
-  BoxCull box;
 };
 // The pool kernel's scans prefetch up to two records past the last quad or
 // prefilter record; these must stay inside DevScene (values never used).
@@ -367,8 +341,6 @@ enum DbgCounter {
   kDbgCyclesDiel,        //   s_memtime cycles in it
   kDbgLightVisits,       // light hits (the path ends with an emission)
   kDbgLightLanes,
-  kDbgBoxFbSteps,        // bounce steps in which some lane ran the rotated box's exact scan (box cull undecided)
-  kDbgBoxFbLanes,        // lanes that did, summed over all bounce steps
   kDbgCounters
 };
 

@@ -354,14 +354,6 @@ class Device:
         sphere BVH."""
         return int(self._L.rtp_sphere_walk_oct_mask(self.handle))
 
-    def box_cull(self) -> bool:
-        """Whether closest-hit searches cull the current scene's rotated box
-        (include/rtp.h rtp_box_cull, read back from the device scene)."""
-        v = int(self._L.rtp_box_cull(self.handle))
-        if v < 0:
-            raise RuntimeError(f"rtp_box_cull: {v}")
-        return bool(v)
-
     def set_ff_tables(self, policy: str) -> dict:
         """RNG jump-table policy of this context (include/rtp.h rtp_set_ff_tables):
         'auto' (default), 'off', or 'on' (build now: a long-lived renderer).
@@ -383,8 +375,7 @@ class Device:
                       "tail_cycles", "fallback_steps", "fallback_lanes", "refill_visits", "refill_lanes",
                       "hit_visits", "hit_lanes", "gen_visits", "gen_lanes", "cycles_gen", "cycles_pdf", "end_visits",
                       "end_lanes", "ffrad_visits", "ffrad_lanes", "ffrad_rows", "dead_lanes", "diel_visits", "diel_lanes",
-                      "cycles_diel", "light_visits", "light_lanes", "boxfb_steps", "boxfb_lanes",
-                      "max_wave_cycles")
+                      "cycles_diel", "light_visits", "light_lanes", "max_wave_cycles")
 
     def debug_counters(self) -> dict:
         """Pool-kernel counters of the last launch made with RTP_DEBUG_STATS=1."""
