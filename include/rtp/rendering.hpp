@@ -30,18 +30,90 @@
 
 #include <algorithm>
 #include <array>
+#include <cmath>
 #include <cstdint>
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../rtp.h"
 
 namespace rtp {
 
-using Vec3f = std::array<float, 3>;
-using Vec4f = std::array<float, 4>;
+// vtkm::Vec<T, N> as the host code uses it: N components (std::array
+// storage, so a std::vector of them is a plain T array for the C ABI),
+// componentwise arithmetic with scalars and vectors, a scalar fills every
+// component (vtkm::Vec(const T&)), N scalars of any arithmetic type convert
+// one by one (vec3(278/555.0, ...): a double divide, then float).
+template <class T, int N>
+struct Vec : std::array<T, N> {
+  using ComponentType = T;
+  static constexpr int NUM_COMPONENTS = N;
+  Vec() : std::array<T, N>{} {}
+  Vec(const T& v) { this->fill(v); }  // NOLINT: implicit like vtkm::Vec
+  template <class... A, std::enable_if_t<sizeof...(A) == N && (N > 1), int> = 0>
+  Vec(A... a) : std::array<T, N>{{static_cast<T>(a)...}} {}  // NOLINT
+  Vec(const std::array<T, N>& a) : std::array<T, N>(a) {}     // NOLINT
+  Vec& operator=(const T& v) {
+    this->fill(v);
+    return *this;
+  }
+#define RTP_VEC_OP(op)                                                  \
+  friend Vec operator op(const Vec& a, const Vec& b) {                  \
+    Vec r;                                                              \
+    for (int i = 0; i < N; i++) r[i] = a[i] op b[i];                    \
+    return r;                                                           \
+  }                                                                     \
+  friend Vec operator op(const Vec& a, const T& s) {                    \
+    Vec r;                                                              \
+    for (int i = 0; i < N; i++) r[i] = a[i] op s;                       \
+    return r;                                                           \
+  }                                                                     \
+  friend Vec operator op(const T& s, const Vec& a) {                    \
+    Vec r;                                                              \
+    for (int i = 0; i < N; i++) r[i] = s op a[i];                       \
+    return r;                                                           \
+  }
+  RTP_VEC_OP(+)
+  RTP_VEC_OP(-)
+  RTP_VEC_OP(*)
+  RTP_VEC_OP(/)
+#undef RTP_VEC_OP
+};
+using Vec3f = Vec<float, 3>;
+using Vec4f = Vec<float, 4>;
+static_assert(sizeof(Vec3f) == 12 && sizeof(Vec4f) == 16, "Vec: N packed components");
+
+// vtkm::cont::ArrayHandle as the host code uses it: a std::vector with the
+// portal accessors main.cc's save() reads (GetNumberOfValues, ReadPortal().Get).
+template <class T>
+struct ArrayHandle : std::vector<T> {
+  using ValueType = T;
+  using std::vector<T>::vector;
+  ArrayHandle() = default;
+  ArrayHandle(const std::vector<T>& v) : std::vector<T>(v) {}  // NOLINT
+  ArrayHandle& operator=(const std::vector<T>& v) {
+    std::vector<T>::operator=(v);
+    return *this;
+  }
+  struct Portal {
+    const ArrayHandle* a;
+    T Get(int64_t i) const { return (*a)[(size_t)i]; }
+    int64_t GetNumberOfValues() const { return (int64_t)a->size(); }
+  };
+  struct WPortal {
+    ArrayHandle* a;
+    T Get(int64_t i) const { return (*a)[(size_t)i]; }
+    void Set(int64_t i, const T& v) const { (*a)[(size_t)i] = v; }
+    int64_t GetNumberOfValues() const { return (int64_t)a->size(); }
+  };
+  int64_t GetNumberOfValues() const { return (int64_t)this->size(); }
+  void Allocate(int64_t n) { this->resize((size_t)n); }
+  Portal ReadPortal() const { return Portal{this}; }
+  WPortal WritePortal() { return WPortal{this}; }
+};
 
 struct ErrorBadValue : std::invalid_argument {
   using std::invalid_argument::invalid_argument;
@@ -80,6 +152,7 @@ struct CellSet {
   std::vector<std::array<int32_t, 4>> quads;
   std::vector<int32_t> spheres;
   std::vector<float> radii;
+  std::vector<int32_t> quadCells;  // QuadIds[0]: the cell id of each quad (the quad mappers' field lookup)
 };
 using CoordinateSystem = std::vector<Vec3f>;
 
@@ -91,9 +164,11 @@ struct Field {
 
 struct DataSet {
   CellSet cells;
+  CoordinateSystem coords;
   std::vector<int32_t> quadCells;  // QuadIds[0]: the cell id of each quad
   std::vector<Field> fields;
   const CellSet& GetCellSet() const { return cells; }
+  const CoordinateSystem& GetCoordinateSystem() const { return coords; }
   const Field& GetField(const std::string& name) const {
     for (const Field& f : fields)
       if (f.name == name) return f;
@@ -140,6 +215,8 @@ struct CornellBox {
     int32_t nf = 0, nq = 0;
     Check(rtp_cornell_point_field(variant, &fv, &nf, &qc, &nq));
     ds.quadCells.assign(qc, qc + nq);
+    ds.cells.quadCells = ds.quadCells;
+    ds.coords = coord;
     ds.fields.assign(1, Field{"point_var", std::vector<float>(fv, fv + nf)});  // CornellBox.cpp:411-416
   }
 };
@@ -179,29 +256,24 @@ class Camera {
   std::array<float, 2> clip_{0.01f, 1000.f};
 };
 
+// vtkm::rendering::Canvas: colour buffer Vec4f per pixel, index j*nx + i
+// (row 0 = camera bottom); depth buffer float per pixel (written by the
+// -direct mappers).  The mappers render into a CanvasRayTracer only
+// (MapperPathTracer.cxx:155-172).
 class Canvas {
  public:
   Canvas(int w, int h) : width_(w), height_(h) {
     if (w <= 0 || h <= 0) throw ErrorBadValue("Canvas: width and height must be positive");
+    color_.assign((size_t)w * h, Vec4f{0.f, 0.f, 0.f, 0.f});
+    depth_.assign((size_t)w * h, 1.001f);
   }
   virtual ~Canvas() = default;
   int GetWidth() const { return width_; }
   int GetHeight() const { return height_; }
-
- private:
-  int width_, height_;
-};
-
-// Colour buffer: Vec4f per pixel, index j*nx + i (row 0 = camera bottom);
-// depth buffer: float per pixel (written by the -direct mappers).
-class CanvasRayTracer : public Canvas {
- public:
-  CanvasRayTracer(int w, int h)
-      : Canvas(w, h), color_((size_t)w * h, Vec4f{0.f, 0.f, 0.f, 0.f}), depth_((size_t)w * h, 1.001f) {}
-  std::vector<Vec4f>& GetColorBuffer() { return color_; }
-  const std::vector<Vec4f>& GetColorBuffer() const { return color_; }
-  std::vector<float>& GetDepthBuffer() { return depth_; }
-  const std::vector<float>& GetDepthBuffer() const { return depth_; }
+  ArrayHandle<Vec4f>& GetColorBuffer() { return color_; }
+  const ArrayHandle<Vec4f>& GetColorBuffer() const { return color_; }
+  ArrayHandle<float>& GetDepthBuffer() { return depth_; }
+  const ArrayHandle<float>& GetDepthBuffer() const { return depth_; }
   // Canvas::Clear (VTK-m): colour 0, depth 1.001
   void Clear() {
     std::fill(color_.begin(), color_.end(), Vec4f{0.f, 0.f, 0.f, 0.f});
@@ -209,8 +281,14 @@ class CanvasRayTracer : public Canvas {
   }
 
  private:
-  std::vector<Vec4f> color_;
-  std::vector<float> depth_;
+  int width_, height_;
+  ArrayHandle<Vec4f> color_;
+  ArrayHandle<float> depth_;
+};
+
+class CanvasRayTracer : public Canvas {
+ public:
+  CanvasRayTracer(int w, int h) : Canvas(w, h) {}
 };
 
 using Field = rtp::Field;  // ignored by the path tracer (MapperPathTracer.cxx:356-383)

@@ -86,6 +86,38 @@ def build_cpp(force: bool = False) -> list[str]:
     return built
 
 
+# The reference's own main.cc, compiled UNCHANGED against librtp.so through
+# the VTK-m-named headers of include/vtkm_compat (rtp/vtkm_compat.hpp): read
+# from its place in the reference tree on stdin, so that its quoted includes
+# ("MapperPathTracer.h", "CornellBox.h", "View3D.h", ...) resolve in
+# include/vtkm_compat/ (the compile's working directory) instead of next to
+# it.  Nothing of the reference is copied; the binary is built where the
+# reference exists (this container) and travels to the GPU box like librtp.so.
+REFERENCE_MAIN = os.environ.get("RTP_REFERENCE_MAIN", "/root/reference/main.cc")
+MAIN_UNCHANGED = os.path.join(ROOT, "examples", "main_cc")
+
+
+def build_main_unchanged(force: bool = False):
+    """Build examples/main_cc from the reference's main.cc; None when the
+    reference is absent (the GPU box)."""
+    if not os.path.exists(REFERENCE_MAIN):
+        return None
+    lib = build()
+    compat = os.path.join(ROOT, "include", "vtkm_compat")
+    hdrs = [os.path.join(ROOT, "include", "rtp", f) for f in ("vtkm_compat.hpp", "rendering.hpp")]
+    deps = hdrs + [REFERENCE_MAIN, lib, os.path.join(ROOT, "include", "rtp.h")]
+    if force or not os.path.exists(MAIN_UNCHANGED) or any(
+            os.path.getmtime(d) > os.path.getmtime(MAIN_UNCHANGED) for d in deps):
+        rel = os.path.relpath(HERE, os.path.dirname(MAIN_UNCHANGED))
+        cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-I", compat, "-I", os.path.join(ROOT, "include"),
+               "-x", "c++", "-", "-L", HERE, "-lrtp", f"-Wl,-rpath,$ORIGIN/{rel}", "-o", MAIN_UNCHANGED]
+        with open(REFERENCE_MAIN, "rb") as src:
+            res = subprocess.run(cmd, stdin=src, cwd=compat, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"g++ failed on the unchanged main.cc:\n{res.stderr[-4000:]}")
+    return MAIN_UNCHANGED
+
+
 ASAN_DIR = os.path.join(ROOT, "tests", "cpp", "asan")
 # programs linked against the host-sanitized library sources (not librtp.so)
 ASAN_PROGRAMS = {
@@ -138,3 +170,4 @@ def build_asan(force: bool = False) -> list[str]:
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
     print("\n".join(build_cpp(force="--force" in sys.argv)))
+    print(build_main_unchanged(force="--force" in sys.argv))

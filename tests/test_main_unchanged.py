@@ -1,0 +1,95 @@
+"""The reference's own main.cc, compiled UNCHANGED against librtp.so
+(raytracingtherestofyourlife_amd/build.py build_main_unchanged: main.cc read
+from the reference tree, its VTK-m and reference includes resolved by the
+same-named headers of include/vtkm_compat over include/rtp/vtkm_compat.hpp)
+-- north_star's "drops into main.cc unchanged" (SURVEY.md 8(b)).
+
+CPU: it builds where the reference is present, and without a HIP device it
+fails loudly (the mapper's device error, no image).
+GPU: its path mode writes the oracle's C1 image byte for byte (main.cc's own
+NormalizeFunctor through vtkm::cont::Algorithm::Transform and its own save());
+its -direct mode writes direct/depth/normals/albedo.pnm equal to the oracle's
+quad-mapper renders."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from raytracingtherestofyourlife_amd import build
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def main_cc():
+    exe = build.build_main_unchanged()
+    if exe is None:
+        exe = build.MAIN_UNCHANGED
+        if not os.path.exists(exe):
+            pytest.skip("the reference's main.cc is absent and no prebuilt examples/main_cc exists")
+    return exe
+
+
+def test_main_cc_is_built_from_the_reference_file(main_cc):
+    if not os.path.exists(build.REFERENCE_MAIN):
+        pytest.skip("reference absent (GPU box): the binary was built in the container")
+    # the compat headers are ours; the source is the reference's file, unmodified
+    compat = os.path.join(ROOT, "include", "vtkm_compat")
+    for h in ("MapperPathTracer.h", "CornellBox.h", "View3D.h", "MapperQuad.h", "vtkm/cont/Algorithm.h"):
+        assert os.path.exists(os.path.join(compat, h))
+    assert not os.path.exists(os.path.join(ROOT, "main.cc")) and not os.path.exists(os.path.join(compat, "main.cc"))
+    assert os.path.getmtime(main_cc) >= os.path.getmtime(build.REFERENCE_MAIN)
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a HIP device is present")
+def test_main_cc_fails_loudly_without_device(main_cc, tmp_path):
+    r = subprocess.run([main_cc, "-x", "8", "-y", "8"], cwd=tmp_path, capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0
+    assert "no HIP device" in r.stderr
+    assert not (tmp_path / "output.pnm").exists()
+
+
+def _pnm_bytes(rgb: np.ndarray, nx: int, ny: int) -> bytes:
+    """save() of main.cc:325-384 restated in numpy (test-side checker)."""
+    c = rgb.astype(np.float32)
+    bad = np.isnan(c).any(axis=1)
+    c = np.where(bad[:, None], np.float32(0), c)
+    q = np.trunc(255.99 * c.astype(np.float64)).astype(np.int64)
+    lines = [f"P3\n{nx} {ny} 255"] + [f"{a} {b} {d}" for a, b, d in q]
+    return ("\n".join(lines) + "\n").encode()
+
+
+@pytest.mark.gpu
+def test_main_cc_path_mode_writes_the_c1_golden(main_cc, oracle, tmp_path):
+    z = np.load(os.path.join(ROOT, "tests", "golden", "c1_full.npz"), allow_pickle=False)
+    nx, ny, spp, depth = int(z["nx"]), int(z["ny"]), int(z["spp"]), int(z["depth"])
+    r = subprocess.run([main_cc, "-x", str(nx), "-y", str(ny), "-samplecount", str(spp), "-raydepth", str(depth)],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "Elapsed time" in r.stdout
+    want = np.zeros((nx * ny, 4), dtype=np.float32)
+    want[:, :3] = z["rgb"]
+    want = oracle.normalize(want, spp)
+    assert (tmp_path / "output.pnm").read_bytes() == _pnm_bytes(want[:, :3], nx, ny)
+
+
+@pytest.mark.gpu
+def test_main_cc_direct_mode_matches_the_oracle(main_cc, oracle, tmp_path):
+    import raytracingtherestofyourlife_amd as rtp
+
+    nx, ny = 40, 32
+    r = subprocess.run([main_cc, "-x", str(nx), "-y", str(ny), "-direct"], cwd=tmp_path, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    sc = oracle.cornell_box(0)
+    cmap = oracle.sample_color_table()
+    cam = oracle.direct_setup(sc, nx, ny)
+    for name, aov in (("direct", 1), ("normals", 2), ("albedo", 4)):
+        want, depth = oracle.render_direct(sc, cam, aov, cmap=cmap)
+        rtp.save_pnm(str(tmp_path / "want.pnm"), want, nx, ny)
+        assert (tmp_path / f"{name}.pnm").read_bytes() == (tmp_path / "want.pnm").read_bytes(), name
+    rtp.save_depth_pnm(str(tmp_path / "want.pnm"), depth, nx, ny)
+    assert (tmp_path / "depth.pnm").read_bytes() == (tmp_path / "want.pnm").read_bytes()
