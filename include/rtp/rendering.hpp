@@ -82,6 +82,21 @@ struct Vec : std::array<T, N> {
   RTP_VEC_OP(/)
 #undef RTP_VEC_OP
 };
+// a float Vec with a double scalar computes in double, then rounds each
+// component to float (vtkm's mixed-precision Vec operators: the reference's
+// scene points are vec3(x) / 555.0, CornellBox.cpp)
+template <int N>
+Vec<float, N> operator/(const Vec<float, N>& a, double s) {
+  Vec<float, N> r;
+  for (int i = 0; i < N; i++) r[i] = (float)((double)a[i] / s);
+  return r;
+}
+template <int N>
+Vec<float, N> operator*(const Vec<float, N>& a, double s) {
+  Vec<float, N> r;
+  for (int i = 0; i < N; i++) r[i] = (float)((double)a[i] * s);
+  return r;
+}
 using Vec3f = Vec<float, 3>;
 using Vec4f = Vec<float, 4>;
 static_assert(sizeof(Vec3f) == 12 && sizeof(Vec4f) == 16, "Vec: N packed components");
@@ -153,13 +168,44 @@ struct CellSet {
   std::vector<int32_t> spheres;
   std::vector<float> radii;
   std::vector<int32_t> quadCells;  // QuadIds[0]: the cell id of each quad (the quad mappers' field lookup)
+  std::vector<int64_t> offsets;    // an explicit cell set's point offsets per cell (CellSetExplicit), if built so
+  // (vtkm::cont::DynamicCellSet::Cast<CellSetExplicit<>>() and its offsets, CornellBox::extract)
+  template <class T>
+  const CellSet& Cast() const {
+    return *this;
+  }
+  template <class A, class B>
+  ArrayHandle<int64_t> GetOffsetsArray(A, B) const {
+    return ArrayHandle<int64_t>(offsets);
+  }
+  int64_t GetNumberOfCells() const { return offsets.empty() ? (int64_t)(quads.size() + spheres.size()) : (int64_t)offsets.size() - 1; }
 };
-using CoordinateSystem = std::vector<Vec3f>;
+// vtkm::cont::CoordinateSystem: the points, with SetData / GetData().Cast<>()
+struct CoordinateSystem : std::vector<Vec3f> {
+  using std::vector<Vec3f>::vector;
+  CoordinateSystem() = default;
+  CoordinateSystem(const std::vector<Vec3f>& v) : std::vector<Vec3f>(v) {}  // NOLINT
+  void SetData(const std::vector<Vec3f>& v) { std::vector<Vec3f>::operator=(v); }
+  struct Data {
+    const CoordinateSystem* c;
+    template <class T>
+    T Cast() const {
+      return T(c->begin(), c->end());
+    }
+  };
+  Data GetData() const { return Data{this}; }
+  int64_t GetNumberOfPoints() const { return (int64_t)size(); }
+};
 
 // vtkm::cont::Field with point association: one value per entry.
 struct Field {
+  enum struct Association { ANY, WHOLE_MESH, POINTS, CELL_SET };
   std::string name;
   std::vector<float> values;
+  Field() = default;
+  Field(std::string n, std::vector<float> v) : name(std::move(n)), values(std::move(v)) {}
+  Field(std::string n, Association, const std::vector<float>& v) : name(std::move(n)), values(v) {}
+  const std::string& GetName() const { return name; }
 };
 
 struct DataSet {
@@ -169,6 +215,14 @@ struct DataSet {
   std::vector<Field> fields;
   const CellSet& GetCellSet() const { return cells; }
   const CoordinateSystem& GetCoordinateSystem() const { return coords; }
+  void AddField(const Field& f) {
+    for (Field& g : fields)
+      if (g.name == f.name) {
+        g = f;
+        return;
+      }
+    fields.push_back(f);
+  }
   const Field& GetField(const std::string& name) const {
     for (const Field& f : fields)
       if (f.name == name) return f;
@@ -320,9 +374,15 @@ class MapperPathTracer {
                    std::vector<int32_t>& matType, std::vector<int32_t>& texType, std::vector<Vec3f>& tex,
                    std::shared_ptr<Device> device = nullptr, int device_ordinal = 0)
       : samplecount(sc), depthcount(dc), MatIdx(matIdx), TexIdx(texIdx), MatType(matType), TexType(texType),
-        Tex(tex), internals_(std::make_shared<Internals>(Internals{std::move(device), device_ordinal, nullptr, true})) {
+        Tex(tex), internals_(std::make_shared<Internals>(Internals{std::move(device), device_ordinal, nullptr, true, {}})) {
     if (!matIdx || !texIdx) throw ErrorBadValue("MapperPathTracer: matIdx/texIdx must point to two index lists");
   }
+  // The reference's own index arrays (vtkm::Id: 64-bit, CornellBox.h:13-14),
+  // narrowed once into lists the mapper owns.
+  MapperPathTracer(int sc, int dc, ArrayHandle<int64_t>* matIdx, ArrayHandle<int64_t>* texIdx,
+                   std::vector<int32_t>& matType, std::vector<int32_t>& texType, std::vector<Vec3f>& tex,
+                   std::shared_ptr<Device> device = nullptr, int device_ordinal = 0)
+      : MapperPathTracer(sc, dc, Narrow(matIdx, texIdx), matType, texType, tex, std::move(device), device_ordinal) {}
 
   // MapperPathTracer.cxx:155-172
   void SetCanvas(Canvas* canvas) {
@@ -370,7 +430,23 @@ class MapperPathTracer {
     int ordinal;
     CanvasRayTracer* canvas;
     bool composite_background;
+    std::shared_ptr<std::vector<int32_t>> owned_idx;  // narrowed matIdx[0..1], texIdx[0..1] (64-bit inputs)
   };
+  using OwnedIdx = std::shared_ptr<std::vector<int32_t>>;
+  static OwnedIdx Narrow(const ArrayHandle<int64_t>* m, const ArrayHandle<int64_t>* t) {
+    if (!m || !t) throw ErrorBadValue("MapperPathTracer: matIdx/texIdx must point to two index lists");
+    OwnedIdx o(new std::vector<int32_t>[4], std::default_delete<std::vector<int32_t>[]>());
+    for (int k = 0; k < 2; k++) {
+      o.get()[k].assign(m[k].begin(), m[k].end());
+      o.get()[2 + k].assign(t[k].begin(), t[k].end());
+    }
+    return o;
+  }
+  MapperPathTracer(int sc, int dc, OwnedIdx own, std::vector<int32_t>& matType, std::vector<int32_t>& texType,
+                   std::vector<Vec3f>& tex, std::shared_ptr<Device> device, int device_ordinal)
+      : MapperPathTracer(sc, dc, own.get(), own.get() + 2, matType, texType, tex, std::move(device), device_ordinal) {
+    internals_->owned_idx = std::move(own);
+  }
 
   rtp_context* device() {
     if (!internals_->device) internals_->device = std::make_shared<Device>(internals_->ordinal);

@@ -386,8 +386,7 @@ void rtpo_cornell_box(int32_t variant, rtpo_scene* s) {
   cb_quad(s, &cell, p, 1, 2, 2);
   /* yz_rect x=0 red (:189-200); first point is vec3(0,0,0) undivided */
   set4(p, 0, 0, 0, 0, 555, 0, 0, 555, 555, 0, 0, 555);
-  cb_quad(s, &cell, p, 1, 0, 0);
-  s->field[s->n_field++] = 1.0f; /* the red wall pushes a fifth value (:196-200) */
+  cb_quad(s, &cell, p, 1, 0, 0); /* four field values (:197-200), like every quad: 89 for 89 points */
   /* light (:204-215) */
   set4(p, 213, 554, 227, 343, 554, 227, 343, 554, 332, 213, 554, 332);
   cb_quad(s, &cell, p, 1, 3, 3);

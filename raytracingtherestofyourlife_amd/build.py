@@ -86,35 +86,56 @@ def build_cpp(force: bool = False) -> list[str]:
     return built
 
 
-# The reference's own main.cc, compiled UNCHANGED against librtp.so through
-# the VTK-m-named headers of include/vtkm_compat (rtp/vtkm_compat.hpp): read
-# from its place in the reference tree on stdin, so that its quoted includes
-# ("MapperPathTracer.h", "CornellBox.h", "View3D.h", ...) resolve in
-# include/vtkm_compat/ (the compile's working directory) instead of next to
-# it.  Nothing of the reference is copied; the binary is built where the
-# reference exists (this container) and travels to the GPU box like librtp.so.
-REFERENCE_MAIN = os.environ.get("RTP_REFERENCE_MAIN", "/root/reference/main.cc")
+# The reference's own main.cc and CornellBox.cpp, compiled UNCHANGED against
+# librtp.so through the VTK-m-named headers of include/vtkm_compat
+# (rtp/vtkm_compat.hpp): each read from its place in the reference tree on
+# stdin, so that its quoted includes ("MapperPathTracer.h", "View3D.h",
+# "pathtracing/SphereExtractor.h", ...) resolve in include/vtkm_compat/ (the
+# compile's working directory) first; "CornellBox.h" and the
+# "pathtracing/vec3.h" it includes are the reference's own (-iquote).
+# Nothing of the reference is copied; the binaries are built where the
+# reference exists (this container) and travel to the GPU box like librtp.so.
+REFERENCE_DIR = os.environ.get("RTP_REFERENCE_DIR", "/root/reference")
+REFERENCE_MAIN = os.path.join(REFERENCE_DIR, "main.cc")
+REFERENCE_SOURCES = ("main.cc", "CornellBox.cpp")
 MAIN_UNCHANGED = os.path.join(ROOT, "examples", "main_cc")
+SCENE_CHECK = os.path.join(ROOT, "tests", "cpp", "scene_unchanged_check")
 
 
 def build_main_unchanged(force: bool = False):
-    """Build examples/main_cc from the reference's main.cc; None when the
-    reference is absent (the GPU box)."""
-    if not os.path.exists(REFERENCE_MAIN):
+    """Build examples/main_cc from the reference's main.cc + CornellBox.cpp,
+    and tests/cpp/scene_unchanged_check (the reference's CornellBox against
+    rtp_cornell_box); None when the reference is absent (the GPU box)."""
+    if not all(os.path.exists(os.path.join(REFERENCE_DIR, f)) for f in REFERENCE_SOURCES):
         return None
     lib = build()
     compat = os.path.join(ROOT, "include", "vtkm_compat")
-    hdrs = [os.path.join(ROOT, "include", "rtp", f) for f in ("vtkm_compat.hpp", "rendering.hpp")]
-    deps = hdrs + [REFERENCE_MAIN, lib, os.path.join(ROOT, "include", "rtp.h")]
-    if force or not os.path.exists(MAIN_UNCHANGED) or any(
-            os.path.getmtime(d) > os.path.getmtime(MAIN_UNCHANGED) for d in deps):
-        rel = os.path.relpath(HERE, os.path.dirname(MAIN_UNCHANGED))
-        cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-I", compat, "-I", os.path.join(ROOT, "include"),
-               "-x", "c++", "-", "-L", HERE, "-lrtp", f"-Wl,-rpath,$ORIGIN/{rel}", "-o", MAIN_UNCHANGED]
-        with open(REFERENCE_MAIN, "rb") as src:
-            res = subprocess.run(cmd, stdin=src, cwd=compat, capture_output=True, text=True)
-        if res.returncode != 0:
-            raise RuntimeError(f"g++ failed on the unchanged main.cc:\n{res.stderr[-4000:]}")
+    inc = os.path.join(ROOT, "include")
+    hdrs = [os.path.join(inc, "rtp", f) for f in ("vtkm_compat.hpp", "rendering.hpp")] + [os.path.join(inc, "rtp.h")]
+    cxx = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-I", compat, "-I", inc, "-iquote", REFERENCE_DIR]
+    objdir = os.path.join(ROOT, "examples", "obj")
+    os.makedirs(objdir, exist_ok=True)
+    objs = {}
+    for f in REFERENCE_SOURCES:
+        src = os.path.join(REFERENCE_DIR, f)
+        obj = os.path.join(objdir, f + ".o")
+        if force or not os.path.exists(obj) or any(os.path.getmtime(d) > os.path.getmtime(obj) for d in hdrs + [src]):
+            with open(src, "rb") as fh:
+                res = subprocess.run(cxx + ["-x", "c++", "-", "-c", "-o", obj], stdin=fh, cwd=compat,
+                                     capture_output=True, text=True)
+            if res.returncode != 0:
+                raise RuntimeError(f"g++ failed on the unchanged {f}:\n{res.stderr[-4000:]}")
+        objs[f] = obj
+    targets = {MAIN_UNCHANGED: [objs["main.cc"], objs["CornellBox.cpp"]],
+               SCENE_CHECK: [os.path.join(ROOT, "tests", "cpp", "scene_unchanged_check.cpp"), objs["CornellBox.cpp"]]}
+    for exe, ins in targets.items():
+        deps = ins + hdrs + [lib]
+        if force or not os.path.exists(exe) or any(os.path.getmtime(d) > os.path.getmtime(exe) for d in deps):
+            rel = os.path.relpath(HERE, os.path.dirname(exe))
+            res = subprocess.run(cxx + ins + ["-L", HERE, "-lrtp", f"-Wl,-rpath,$ORIGIN/{rel}", "-o", exe], cwd=compat,
+                                 capture_output=True, text=True)
+            if res.returncode != 0:
+                raise RuntimeError(f"g++ link failed for {exe}:\n{res.stderr[-4000:]}")
     return MAIN_UNCHANGED
 
 

@@ -123,8 +123,7 @@ void build(SceneStore& s, int variant) {
   rect(p, {555, 0, 0, 555, 555, 0, 555, 555, 555, 555, 0, 555});  // green wall (:175-186)
   s.add_quad(p, 2, 2);
   rect(p, {0, 0, 0, 0, 555, 0, 0, 555, 555, 0, 0, 555});  // red wall (:189-200)
-  s.add_quad(p, 0, 0);
-  s.field.push_back(1.f);  // the red wall pushes a fifth field value (:196-200)
+  s.add_quad(p, 0, 0);  // (four field values like every quad, :197-200: 89 values for the 89 points)
   rect(p, {213, 554, 227, 343, 554, 227, 343, 554, 332, 213, 554, 332});  // light (:204-215)
   s.add_quad(p, 3, 3);
   rect(p, {0, 555, 0, 555, 555, 0, 555, 555, 555, 0, 555, 555});  // ceiling

@@ -1,11 +1,16 @@
-"""The reference's own main.cc, compiled UNCHANGED against librtp.so
-(raytracingtherestofyourlife_amd/build.py build_main_unchanged: main.cc read
-from the reference tree, its VTK-m and reference includes resolved by the
-same-named headers of include/vtkm_compat over include/rtp/vtkm_compat.hpp)
--- north_star's "drops into main.cc unchanged" (SURVEY.md 8(b)).
+"""The reference's own main.cc and CornellBox.cpp, compiled UNCHANGED against
+librtp.so (raytracingtherestofyourlife_amd/build.py build_main_unchanged:
+both read from the reference tree, their VTK-m and reference includes
+resolved by the same-named headers of include/vtkm_compat over
+include/rtp/vtkm_compat.hpp; CornellBox.h and pathtracing/vec3.h are the
+reference's own) -- north_star's "drops into main.cc unchanged" (SURVEY.md
+8(b)).
 
-CPU: it builds where the reference is present, and without a HIP device it
-fails loudly (the mapper's device error, no image).
+CPU: they build where the reference is present; the reference's CornellBox,
+built by its own code over the shim, equals the library's scene bit for bit
+(points, quads, sphere, tables, the point field and the quad cell ids:
+tests/cpp/scene_unchanged_check.cpp); without a HIP device main_cc fails
+loudly (the mapper's device error, no image).
 GPU: its path mode writes the oracle's C1 image byte for byte (main.cc's own
 NormalizeFunctor through vtkm::cont::Algorithm::Transform and its own save());
 its -direct mode writes direct/depth/normals/albedo.pnm equal to the oracle's
@@ -38,10 +43,21 @@ def test_main_cc_is_built_from_the_reference_file(main_cc):
         pytest.skip("reference absent (GPU box): the binary was built in the container")
     # the compat headers are ours; the source is the reference's file, unmodified
     compat = os.path.join(ROOT, "include", "vtkm_compat")
-    for h in ("MapperPathTracer.h", "CornellBox.h", "View3D.h", "MapperQuad.h", "vtkm/cont/Algorithm.h"):
+    for h in ("MapperPathTracer.h", "View3D.h", "MapperQuad.h", "vtkm/cont/Algorithm.h",
+              "vtkm/cont/DataSetBuilderExplicit.h", "pathtracing/SphereExtractor.h", "vtkm/Transform3D.h"):
         assert os.path.exists(os.path.join(compat, h))
-    assert not os.path.exists(os.path.join(ROOT, "main.cc")) and not os.path.exists(os.path.join(compat, "main.cc"))
+    # the reference's own CornellBox.h and sources; no copy of them in the repo
+    for f in ("CornellBox.h", "main.cc", "CornellBox.cpp"):
+        assert not os.path.exists(os.path.join(compat, f)) and not os.path.exists(os.path.join(ROOT, f))
     assert os.path.getmtime(main_cc) >= os.path.getmtime(build.REFERENCE_MAIN)
+
+
+def test_reference_cornellbox_equals_the_library_scene(main_cc):
+    if not os.path.exists(build.SCENE_CHECK):
+        pytest.skip("tests/cpp/scene_unchanged_check was not built (reference absent)")
+    r = subprocess.run([build.SCENE_CHECK], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().splitlines()[-1] == "OK"
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a HIP device is present")
