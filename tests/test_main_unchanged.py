@@ -10,7 +10,10 @@ CPU: they build where the reference is present; the reference's CornellBox,
 built by its own code over the shim, equals the library's scene bit for bit
 (points, quads, sphere, tables, the point field and the quad cell ids:
 tests/cpp/scene_unchanged_check.cpp); without a HIP device main_cc fails
-loudly (the mapper's device error, no image).
+loudly (the mapper's device error, no image).  The scene check tests the
+boundary (the reference's scene code through our API builds our scene); it
+does not pin the oracle -- a build over VTK-m stand-ins is not a reference
+build, and the oracle's parity claims rest on tests/golden alone.
 GPU: its path mode writes the oracle's C1 image byte for byte (main.cc's own
 NormalizeFunctor through vtkm::cont::Algorithm::Transform and its own save());
 its -direct mode writes direct/depth/normals/albedo.pnm equal to the oracle's
