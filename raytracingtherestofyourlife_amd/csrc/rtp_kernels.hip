@@ -587,6 +587,13 @@ RTP_DEV int bounce(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed, f3
     dbg[kDbgFallbackSteps] += m ? 1 : 0;
     dbg[kDbgFallbackLanes] += (unsigned long long)__popcll(m);
   }
+  if (gdbg) {  // (stats) lanes whose closest hit is one of the exact-scan quads (kinds 7..10, 0)
+    const uint64_t mb = __ballot(h.kind == 0 && h.idx >= sc->kind_begin[6]);
+    if ((int)(threadIdx.x & 63) == (int)__builtin_ctzll(__ballot(true))) {
+      if (mb == 0) dbg_add(gdbg, kDbgBoxFreeSteps, 1ull);
+      dbg_add(gdbg, kDbgBoxLanes, (unsigned long long)__popcll(mb));
+    }
+  }
   if (st) {
     const unsigned long long t1s = __builtin_amdgcn_s_memtime();
     dbg[kDbgCyclesIntersect] += t1s - t0;

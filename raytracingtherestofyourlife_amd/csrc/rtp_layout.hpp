@@ -341,6 +341,9 @@ enum DbgCounter {
   kDbgCyclesDiel,        //   s_memtime cycles in it
   kDbgLightVisits,       // light hits (the path ends with an emission)
   kDbgLightLanes,
+  kDbgBoxFreeSteps,      // bounce steps in which no live lane's closest hit is an exact-scan quad (the
+                         //   rotated box's faces): the most a wave-uniform box reject could skip (r06)
+  kDbgBoxLanes,          // live lanes whose closest hit is one, summed over bounce steps
   kDbgCounters
 };
 

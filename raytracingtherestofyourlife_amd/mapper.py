@@ -375,7 +375,8 @@ class Device:
                       "tail_cycles", "fallback_steps", "fallback_lanes", "refill_visits", "refill_lanes",
                       "hit_visits", "hit_lanes", "gen_visits", "gen_lanes", "cycles_gen", "cycles_pdf", "end_visits",
                       "end_lanes", "ffrad_visits", "ffrad_lanes", "ffrad_rows", "dead_lanes", "diel_visits", "diel_lanes",
-                      "cycles_diel", "light_visits", "light_lanes", "max_wave_cycles")
+                      "cycles_diel", "light_visits", "light_lanes", "box_free_steps", "box_lanes",
+                      "max_wave_cycles")
 
     def debug_counters(self) -> dict:
         """Pool-kernel counters of the last launch made with RTP_DEBUG_STATS=1."""
