@@ -137,6 +137,9 @@ int main(int argc, char** argv) {
       }
     };
     if (hemi) {
+      // generateHemisphere's own camera: near plane 1, not main()'s 0.1
+      // (main.cc:519 `SetClippingRange(01.f, 5.f)`; it moves the depth AOV)
+      cam.SetClippingRange(1.0f, 5.f);
       for (const View& w : views) {
         char suffix[64];
         std::snprintf(suffix, sizeof(suffix), "-%.4f-%.4f", w.phi, w.theta);

@@ -171,7 +171,7 @@ def test_hemisphere_direct_views_like_oracle(programs, oracle, tmp_path):
     cmap = oracle.sample_color_table()
     for name, pos_bits in _hemisphere_plan_py(2, 2):
         pos = np.array(pos_bits, dtype=np.uint32).view(np.float32)
-        cam = oracle.direct_setup(sc, nx, ny, position=pos)
+        cam = oracle.direct_setup(sc, nx, ny, position=pos, clip=(1.0, 5.0))  # main.cc:519
         for prefix, aov in (("direct", 1), ("normals", 2), ("albedo", 4)):
             want, depth = oracle.render_direct(sc, cam, aov, cmap=cmap)
             rtp.save_pnm(str(tmp_path / "want.pnm"), want, nx, ny)

@@ -112,3 +112,53 @@ def test_main_cc_direct_mode_matches_the_oracle(main_cc, oracle, tmp_path):
         assert (tmp_path / f"{name}.pnm").read_bytes() == (tmp_path / "want.pnm").read_bytes(), name
     rtp.save_depth_pnm(str(tmp_path / "want.pnm"), depth, nx, ny)
     assert (tmp_path / "depth.pnm").read_bytes() == (tmp_path / "want.pnm").read_bytes()
+
+
+@pytest.mark.gpu
+def test_main_cc_hemisphere_views_match_the_oracle(main_cc, oracle, tmp_path):
+    """main.cc's -hemisphere mode (generateHemisphere, main.cc:504-561, and
+    generate(), :387-429) run unchanged: one output-<phi>-<theta>.pnm per view,
+    the camera moved on its sphere by main.cc's own float arithmetic (its
+    cos/sin resolve to the float overloads: the binary calls sincosf), the
+    canvas reused across views.  Each image is main.cc's save() of the
+    oracle's render of that view."""
+    from test_cpp_host import _hemisphere_plan_py
+
+    nx, ny, spp, depth = 24, 16, 3, 6
+    r = subprocess.run([main_cc, "-hemisphere", "-phicount", "2", "-thetacount", "2", "-x", str(nx), "-y", str(ny),
+                        "-samplecount", str(spp), "-raydepth", str(depth)], cwd=tmp_path, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    views = _hemisphere_plan_py(2, 2)
+    assert sorted(p.name for p in tmp_path.glob("output-*.pnm")) == sorted(f"output-{n}.pnm" for n, _ in views)
+    sc = oracle.cornell_box(0)
+    for name, pos_bits in views:
+        pos = np.array(pos_bits, dtype=np.uint32).view(np.float32)
+        cam = oracle.camera_setup(nx, ny, position=pos)
+        want, _, _ = oracle.render_pixels(sc, cam, nx, ny, spp, depth, np.arange(nx * ny, dtype=np.int64))
+        want = oracle.normalize(want, spp)
+        assert (tmp_path / f"output-{name}.pnm").read_bytes() == _pnm_bytes(want[:, :3], nx, ny), name
+
+
+@pytest.mark.gpu
+def test_main_cc_hemisphere_direct_views_match_the_oracle(main_cc, oracle, tmp_path):
+    """-hemisphere -direct: direct-, depth-, normals- and albedo-<phi>-<theta>.pnm
+    per view (main.cc:402-421), each the oracle's quad-mapper render of that view."""
+    import raytracingtherestofyourlife_amd as rtp
+    from test_cpp_host import _hemisphere_plan_py
+
+    nx, ny = 20, 18
+    r = subprocess.run([main_cc, "-hemisphere", "-phicount", "2", "-thetacount", "2", "-x", str(nx), "-y", str(ny),
+                        "-direct"], cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    sc = oracle.cornell_box(0)
+    cmap = oracle.sample_color_table()
+    for name, pos_bits in _hemisphere_plan_py(2, 2):
+        pos = np.array(pos_bits, dtype=np.uint32).view(np.float32)
+        cam = oracle.direct_setup(sc, nx, ny, position=pos, clip=(1.0, 5.0))  # main.cc:519
+        for prefix, aov in (("direct", 1), ("normals", 2), ("albedo", 4)):
+            want, dep = oracle.render_direct(sc, cam, aov, cmap=cmap)
+            rtp.save_pnm(str(tmp_path / "want.pnm"), want, nx, ny)
+            assert (tmp_path / f"{prefix}-{name}.pnm").read_bytes() == (tmp_path / "want.pnm").read_bytes(), (prefix, name)
+        rtp.save_depth_pnm(str(tmp_path / "want.pnm"), dep, nx, ny)
+        assert (tmp_path / f"depth-{name}.pnm").read_bytes() == (tmp_path / "want.pnm").read_bytes(), name
