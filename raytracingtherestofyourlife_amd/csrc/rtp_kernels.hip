@@ -644,14 +644,30 @@ RTP_DEV int shade_hit(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed,
     return kLight;
   }
   f3 atten;
-  if (mt == 2) {  // DielectricWorklet: 1 draw before generation, specular
+  // The RNG draws of both scattering materials, taken together (one pass for
+  // the dielectric and Lambertian lanes instead of one per branch): the
+  // dielectric's own draw (DielectricWorklet, EmitWorklet.h), then for both
+  // the which draw and the generator's 2 / 3 / 2 draws (PdfWorklet.h:20,
+  // 63-213; a dielectric discards the direction: dead_step's advance) and
+  // SpherePDFWorklet's discarded draw (no draw lies between the generator and
+  // it: quad_pdf_value draws none).
+  const bool glass = mt == 2;
+  float rglass = 0.0f;
+  if (glass) rglass = randf(seed);
+  const uint32_t tw = wang(seed);  // which (PdfWorklet.h:20)
+  seed = tw;
+  const bool is_cos = tw < t1, is_quad = !is_cos && tw < t2;
+  const float ra = randf(seed);
+  const float rb = randf(seed);
+  uint32_t s3 = seed;
+  const float rc = randf(s3);
+  seed = is_quad ? s3 : seed;
+  (void)randf(seed);  // SpherePDFWorklet's discarded draw
+  if (glass) {  // DielectricWorklet: specular
     const unsigned long long td0 = stamp(dbg != nullptr);
     if (dbg) dbg_region(dbg, kDbgDielVisits);
-    float r = randf(seed);
     f3 sd;
-    dielectric_scatter(dir, hn, sc->ior, sc->ior_r0sq, sc->ior_inv, r, sd);
-    seed = dead_step(seed, t1, t2);  // generation draws (direction unused)
-    (void)randf(seed);               // SpherePDFWorklet's discarded draw
+    dielectric_scatter(dir, hn, sc->ior, sc->ior_r0sq, sc->ior_inv, rglass, sd);
     atten = mk(1.f, 1.f, 1.f);
     ps.org = hp;
     ps.dir = sd;
@@ -664,20 +680,12 @@ RTP_DEV int shade_hit(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed,
     if (dbg) dbg_region(dbg, kDbgGenVisits);
     f3 gen;
     float sph_ctm = -1.0f;  // sqrt(1 - R^2/|c-hp|^2) when the generator made it (sphere_pdf_value reuses it)
-    uint32_t tw = wang(seed);  // which (PdfWorklet.h:20)
-    seed = tw;
     // The three generators as one branch-free pass.  Cosine (PdfWorklet.h:
     // 63-79) and light-sphere (:193-213) directions share the ONB, the
     // sincos of phi = 2*pi*r1 and local(); they differ in w, in which draw
     // is r1 (g++ evaluates the sphere generator's draws right to left), and
     // in z and the radial factor.  The light-quad point (:112-137) needs a
-    // third draw, taken only by its lanes.
-    const bool is_cos = tw < t1, is_quad = !is_cos && tw < t2;
-    const float ra = randf(seed);
-    const float rb = randf(seed);
-    uint32_t s3 = seed;
-    const float rc = randf(s3);
-    seed = is_quad ? s3 : seed;
+    // third draw, taken only by its lanes (drawn above).
     const f3 rp = mk(L.gx0 + ra * L.gdx, L.gy0 + rb * L.gdy, L.gz0 + rc * L.gdz);
     const f3 genq = sub(rp, hp);
     const f3 direction = sub(ld3(L.sc), hp);
@@ -704,8 +712,7 @@ RTP_DEV int shade_hit(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed,
     // 1/|gen| once: QuadPDFWorklet's rmag and both unit_vector(gen) below
     const float rg = rmag(gen);
     sum += weight * quad_pdf_value(L, hp, gen, rg);
-    (void)randf(seed);
-    sum += weight * sphere_pdf_value(L, hp, gen, sph_ctm);
+    sum += weight * sphere_pdf_value(L, hp, gen, sph_ctm);  // (its discarded draw: above)
     // PDFCosineWorklet (ScatterWorklet.h:96-112): mixture in double
     const f3 ug = scl(gen, rg);       // unit_vector(gen)
     const f3 w_hn = unit_vector(hn);  // build_from_w(hn).w (u and v are unused here)
