@@ -98,7 +98,6 @@ void fill_quad(rtp::DevQuad& Q, v3 q, v3 r, v3 s, v3 t) {
   st(Q.e21, sub(r, s));
   st(Q.e23, sub(t, s));
   st(Q.n, normalize(cross(sub(r, q), sub(s, q))));  // TriangleNormal(q,r,s), Surface.h:182-183
-  st(Q.w, normalize(ld(Q.n)));                       // build_from_w(n).w (onb.h:34-36), the device's unit_vector
   // zero-structure kind (exact zeros only; see quad_hit_masked)
   auto mask_of = [](const float* e) {
     int m = 0;
@@ -756,7 +755,6 @@ rtp_status rtp_set_scene(rtp_context* c, const rtp_scene_desc* s) {
     st(S.c, ld(s->points + 3 * s->sphere_point[k]));
     S.r = s->sphere_radius[k];
     S.rr = S.r * S.r;
-    S.rinv = (std::fabs(S.r) >= 0x1p-20f && std::fabs(S.r) <= 0x1p20f) ? 1.0f / S.r : 0.0f;  // IEEE: RN(1/r)
     S.mt = s->mat_type[s->sphere_mat[k]];
     st(S.alb, ld(s->tex_rgb + 3 * s->tex_type[s->sphere_tex[k]]));
   }

@@ -58,12 +58,6 @@ constexpr int kHistChunk = RTP_HIST_CHUNK;
 #ifndef RTP_CRIT_FF
 #define RTP_CRIT_FF 100  // pool kernel: lag (per mille of the wave's average samples) that makes a pixel critical
 #endif
-#ifndef RTP_SPH_NORMAL_MK
-#define RTP_SPH_NORMAL_MK 1  // sphere hit normals as Markstein divisions by RN(1/r) (shade_hit)
-#endif
-#ifndef RTP_LDS_ADD
-#define RTP_LDS_ADD 1  // path end: the slot's sample and live counts as LDS adds without return
-#endif
 
 namespace rtp {
 
@@ -294,10 +288,7 @@ RTP_DEV void spheres_bvh(const DevScene* __restrict__ sc, f3 o, f3 d, Hit& h) {
 // Every quad of a scene (kMaxQuads, 8 KiB): with a table that could be
 // absent, the compiler merged the LDS and global reads of the hit's record
 // into 7 flat loads (waited on both counters); now they are 2 ds_read_b128.
-#ifndef RTP_QUAD_W
-#define RTP_QUAD_W 1  // a Lambertian quad hit's ONB w from the table (DevQuad::w) instead of unit_vector(hn)
-#endif
-constexpr int kLdsQuads = kMaxQuads, kQShadeFloats = RTP_QUAD_W ? 12 : 8;  // per quad: n, alb, mt, pad (, w, pad)
+constexpr int kLdsQuads = kMaxQuads, kQShadeFloats = 8;  // per quad: n, alb, mt, pad
 // The block's LDS table also holds the prefilter's PreExact records (after
 // the shading data): the candidate's record is then 4 ds_read_b128 instead of
 // 4 global loads (L2 hits) on every bounce's critical path (C2 kernel -1.7%,
@@ -309,7 +300,7 @@ RTP_DEV void fill_qshade(const DevScene* __restrict__ sc, float* s_qshade) {
   for (int i = threadIdx.x; i < sc->n_quads * kQShadeFloats; i += blockDim.x) {
     const DevQuad& Q = sc->quads[i / kQShadeFloats];
     const int f = i % kQShadeFloats;
-    s_qshade[i] = f < 3 ? Q.n[f] : f < 6 ? Q.alb[f - 3] : f == 6 ? __int_as_float(Q.mt) : f >= 8 && f < 11 ? Q.w[f - 8] : 0.f;
+    s_qshade[i] = f < 3 ? Q.n[f] : f < 6 ? Q.alb[f - 3] : f == 6 ? __int_as_float(Q.mt) : 0.f;
   }
   const float* px = reinterpret_cast<const float*>(sc->prex);
   for (int i = threadIdx.x; i < sc->n_pre * 16; i += blockDim.x) s_qshade[kPrexLdsOffset + i] = px[i];
@@ -630,7 +621,6 @@ RTP_DEV int shade_hit(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed,
   f3 hn;
   int mt;
   f3 alb;
-  f3 wq = mk(0.f, 0.f, 0.f);  // (RTP_QUAD_W, quad hits) unit_vector(hn) from the table
   if (h.kind == 0) {
     // (an LDS table always: a global fallback here made the compiler read
     // both through one flat pointer)
@@ -639,37 +629,10 @@ RTP_DEV int shade_hit(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed,
     hn = mk(r0.x, r0.y, r0.z);
     alb = mk(r0.w, r1.x, r1.y);
     mt = __float_as_int(r1.z);
-#if RTP_QUAD_W
-    const float4 r2 = r[2];
-    wq = mk(r2.x, r2.y, r2.z);
-    if (dot(hn, dir) > 0.f) {  // Surface.h:184-185
-      hn = neg(hn);
-      wq = neg(wq);
-    }
-#else
     if (dot(hn, dir) > 0.f) hn = neg(hn);  // Surface.h:184-185
-#endif
   } else {
     const DevSphere& S = kBvh ? sc->sph_all[h.idx] : sc->spheres[h.idx];
-    const f3 a = mk(hp.x - S.c[0], hp.y - S.c[1], hp.z - S.c[2]);
-#if RTP_SPH_NORMAL_MK
-    // (p - c) / r (SphereIntersector.h) as Markstein divisions by the host's
-    // RN(1/r): with |a| in [2^-40, 2^40] and r in [2^-20, 2^20] nothing
-    // over- or underflows (a nonzero remainder is a multiple of
-    // ulp(r) ulp(q) >= 2^-126), so each is RN(a / r) (div_markstein).
-    // Zero, tiny or huge components and radii out of range (rinv = 0) take
-    // the IEEE division behind a wave-uniform branch.
-    const float ri = S.rinv;
-    hn = mk(div_markstein(a.x, S.r, ri), div_markstein(a.y, S.r, ri), div_markstein(a.z, S.r, ri));
-    auto in_range = [](float x) { return fabsf(x) >= 0x1p-40f && fabsf(x) <= 0x1p40f; };
-    const bool slow = !(ri != 0.0f && in_range(a.x) && in_range(a.y) && in_range(a.z));
-    if (__ballot(slow)) {
-      asm volatile("");
-      if (slow) hn = mk(a.x / S.r, a.y / S.r, a.z / S.r);
-    }
-#else
-    hn = mk(a.x / S.r, a.y / S.r, a.z / S.r);
-#endif
+    hn = mk((hp.x - S.c[0]) / S.r, (hp.y - S.c[1]) / S.r, (hp.z - S.c[2]) / S.r);
     mt = S.mt;
     alb = ld3(S.alb);
   }
@@ -752,18 +715,7 @@ RTP_DEV int shade_hit(const DevScene* __restrict__ sc, Path& ps, uint32_t& seed,
     sum += weight * sphere_pdf_value(L, hp, gen, sph_ctm);  // (its discarded draw: above)
     // PDFCosineWorklet (ScatterWorklet.h:96-112): mixture in double
     const f3 ug = scl(gen, rg);       // unit_vector(gen)
-#if RTP_QUAD_W
-    // build_from_w(hn).w (u and v are unused here): a quad's from the table
-    // (the host's Normalize(n), the same float operations); spheres compute it
-    f3 w_hn = wq;
-    const bool w_sph = h.kind != 0;
-    if (__ballot(w_sph)) {
-      asm volatile("");
-      if (w_sph) w_hn = unit_vector(hn);
-    }
-#else
     const f3 w_hn = unit_vector(hn);  // build_from_w(hn).w (u and v are unused here)
-#endif
     float cv;
     {
       float cosine = dot(ug, w_hn);
@@ -1398,16 +1350,8 @@ __device__ __forceinline__ void pool_body(const DevScene* __restrict__ sc, const
         // path died there (bounce<.., true> left them to the fast-forward)
         const int rem = D - 1 - k_end + (res != kAlive ? 1 : 0);
         s_rem[slot] = (uint16_t)(rem | (res == kLight ? kEndLight : 0) | (ps.nonfinite ? kEndNonfinite : 0));
-        if constexpr (RTP_LDS_ADD && !kWalk) {
-          // (no other lane touches the slot while its sample is in flight:
-          // LDS adds without return, no read round trip; r06m: C2 -0.5%,
-          // the sphere-BVH instance +1%, so it keeps the read-modify-write)
-          __hip_atomic_fetch_add(s_samples + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-          __hip_atomic_fetch_add(s_live + slot, (uint32_t)(k_end + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        } else {
-          s_samples[slot] = s_samples[slot] + 1u;
-          s_live[slot] = s_live[slot] + (uint32_t)(k_end + 1);
-        }
+        s_samples[slot] = s_samples[slot] + 1u;
+        s_live[slot] = s_live[slot] + (uint32_t)(k_end + 1);
         s_seed[slot] = seed;
         ended = true;
         has_path = false;

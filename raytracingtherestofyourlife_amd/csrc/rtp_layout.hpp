@@ -57,7 +57,7 @@ struct alignas(16) DevQuad {
   float n[3];                    // Normalize(TriangleNormal(q,r,s)), unflipped
   float alb[3];                  // tex[texType[texIdx]]
   int32_t mt;                    // matType[matIdx]
-  float w[3];                    // Normalize(n): the shading ONB's w of a hit (unit_vector(-n) == -w exactly)
+  int32_t pad[3];
 };
 // The scan-time head of a DevQuad (same field offsets).
 struct alignas(16) QuadGeom {
@@ -81,10 +81,8 @@ struct alignas(16) DevSphere {
   float rr;  // radius*radius (Surface.h:328)
   float alb[3];
   int32_t mt;
-  float rinv;  // RN(1/r) for the hit normal's Markstein divisions when r is in [2^-20, 2^20], else 0
-  int32_t pad[6];
+  int32_t pad[7];
 };
-static_assert(sizeof(DevSphere) == 64, "DevSphere: 64 bytes");
 
 // Sphere record in BVH leaf order (global memory, per-lane loads).
 struct alignas(16) DevSphereG {
