@@ -18,8 +18,10 @@ the tile-deal instance the ranks of a tile-sharded run use).
 N > 1 (launched by torch.distributed.run, one process per GPU):
   --scaling strong (default): THE frame, split over the ranks (c2/c4: 16x16
       tiles dealt round-robin; c5: sample batches); the float4
-      framebuffer is summed to rank 0 with ONE reduce per step (RCCL over xGMI),
-      overlapped with the next step's render (two canvases, alternating).
+      framebuffer is summed to rank 0 with ONE reduce per step, a pairwise tree
+      of RCCL point-to-point transfers over xGMI in a fixed association
+      (shard.tree_reduce_: the same bits on any node), overlapped with the next
+      step's render (two canvases, alternating).
   --scaling weak: every rank renders a full nx x ny band of an nx x ny*N
       canvas (per-GPU work fixed).
   After the timed region rank 0 renders the same workload's whole frame alone
@@ -39,7 +41,7 @@ C2 frame (tests/golden/c2_full.npz); at N > 1 the C5 line takes them from
 `reduced_frame_parity`: every rank's shard and the reduced frame at 1024
 pixels against the oracle's reduced-frame fixture of that N
 (tests/golden/c5_reduced.npz, N = 2/4/8; bit-exact shards, the reduced frame
-bit-exact against the shards' sum in the reduce's association), plus the
+bit-exact against the shards' sum in the reduce's fixed association), plus the
 statistical check of the reduced frame against an independent single-stream
 image.  `bench.py --gpus N` without torch.distributed.run starts it (one
 process per GPU) as a child and relays rank 0's line.  `roofline` prices the render kernel
@@ -222,11 +224,11 @@ def _same_bits(a: np.ndarray, b: np.ndarray) -> np.ndarray:
 
 
 def association_sums(shards: np.ndarray) -> dict:
-    """float32 sums of the N shards in the associations a reduce may use: a
-    chain along the ring of ranks from any start k, in either direction
-    (((s_k + s_k+1) + ...) + s_k-1: a ring reduce, and a ring reduce-scatter
-    whose chunk c starts at rank c + 1 -- gloo, or RCCL's channels), and the
-    pairwise tree.  "rank_order" is the forward chain from rank 0."""
+    """float32 sums of the N shards in several associations: the pairwise
+    tree (shard.tree_reduce_'s, the one bench.py's reduce uses) and, for
+    diagnosis, a chain along the ring of ranks from any start k in either
+    direction (((s_k + s_k+1) + ...) + s_k-1: what a ring reduce in rank
+    order would give).  "rank_order" is the forward chain from rank 0."""
     s = [np.asarray(x, np.float32) for x in shards]
     n = len(s)
     if n <= 2:  # one add: the same either way
@@ -240,22 +242,22 @@ def association_sums(shards: np.ndarray) -> dict:
                 acc = acc + s[r]
             name = "rank_order" if (direction, k) == (1, 0) else f"ring_{'fwd' if direction > 0 else 'rev'}_from_{k}"
             out[name] = acc
-    lvl = s
-    while len(lvl) > 1:
-        lvl = [lvl[i] + lvl[i + 1] if i + 1 < len(lvl) else lvl[i] for i in range(0, len(lvl), 2)]
-    out["pairwise_tree"] = lvl[0]
+    from raytracingtherestofyourlife_amd import shard
+
+    out["pairwise_tree"] = shard.tree_sum(s)
     return out
 
 
 def reduced_frame_parity(fix: dict, shards_got: list, reduced_got: np.ndarray, spp: int) -> dict:
     """The N > 1 line's parity against the oracle:
     every rank's shard at the fixture pixels bit for bit against the oracle's
-    shard, and the reduced frame against the oracle's reduced frame -- bit for
-    bit against the oracle shards' float32 sum in some association a reduce
-    may use (two ranks: one add, so exactly the fixture), and the per-pixel
-    RMSE of the normalised frames (NormalizeFunctor, main.cc:253-287) against
-    the fixture's rank-order sum.  shards_got: N arrays [n, >=3]; reduced_got
-    [n, >=3]."""
+    shard, and the reduced frame bit for bit against the oracle's shards
+    summed in float32 in the reduce's own association (shard.tree_reduce_:
+    the pairwise tree; two ranks: one add, so exactly the fixture's
+    rank-order sum), plus the per-pixel RMSE of the normalised frames
+    (NormalizeFunctor, main.cc:253-287) against the fixture's rank-order sum.
+    The other associations are reported for diagnosis.  shards_got: N arrays
+    [n, >=3]; reduced_got [n, >=3]."""
     import raytracingtherestofyourlife_amd as rtp
 
     want = fix["shards"]
@@ -265,6 +267,7 @@ def reduced_frame_parity(fix: dict, shards_got: list, reduced_got: np.ndarray, s
     red = np.ascontiguousarray(reduced_got[:, :3], np.float32)
     sums = association_sums(want)
     per = {k: _same_bits(red, v).all(1) for k, v in sums.items()}
+    own = per["pairwise_tree" if "pairwise_tree" in per else "rank_order"]  # shard.tree_reduce_'s association
     any_match = np.logical_or.reduce(list(per.values()))
     a = np.c_[red, np.zeros(n, np.float32)].astype(np.float32)
     b = np.c_[fix["reduced"], np.zeros(n, np.float32)].astype(np.float32)
@@ -276,12 +279,13 @@ def reduced_frame_parity(fix: dict, shards_got: list, reduced_got: np.ndarray, s
     return {"fixture": fix["name"], "pixels": int(n), "ranks": len(want),
             "shards_bit_exact": all(shard_ok) and len(shard_ok) == len(want),
             "shard_bit_exact_per_rank": shard_ok,
+            "reduced_bit_exact_tree": bool(own.all()),
             "reduced_bit_exact_rank_order": bool(per["rank_order"].all()),
             "reduced_association": {k: int(v.sum()) for k, v in per.items()},
             "reduced_pixels_matching_an_association": int(any_match.sum()),
             "reduced_max_rel_vs_rank_order": float(rel.max()) if rel.size else 0.0,
             "rmse": float(np.sqrt(np.mean(d * d))),
-            "bit_exact": bool(all(shard_ok) and any_match.all())}
+            "bit_exact": bool(all(shard_ok) and own.all())}
 
 
 def load_valu(path: str, cfg: dict, kernel_ms: float):
@@ -628,12 +632,8 @@ def main() -> None:
         red_np = canvas[:, :3].cpu().numpy()
         if samples:
             single = full.index_select(0, torch.from_numpy(chk).cuda()).cpu().numpy()
-            # the shards summed in rank order in float32 (a reduce of two ranks is one add: exact;
-            # more ranks may associate differently)
-            summed = gathered[0][:, :3].copy()
-            for q in gathered[1:]:
-                summed = summed + q[:, :3]
-            summed = summed.astype(np.float64)
+            # the shards summed in float32 in the reduce's association (shard.tree_sum): exact
+            summed = shard.tree_sum([q[:, :3] for q in gathered]).astype(np.float64)
             red_chk = red_np[chk].astype(np.float64)
             # the reduced frame against the single-stream image (shard.sample_shard_ttest: block means of the
             # per-pixel difference, Student-t); both estimate the same radiance

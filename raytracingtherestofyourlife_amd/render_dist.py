@@ -23,8 +23,9 @@ the slowest rank's wall time between two barriers.
 
 --backend gloo --share-gpu rehearses the same code with every rank on device
 0 and a host-side reduce (a one-GPU box).  --check makes rank 0 re-render the
-reference and compare: bit-exact for tiles, the ranks' shard renders summed
-in rank order for samples (rel. 1e-6: RCCL's summation order differs).
+reference and compare: bit-exact for tiles; for samples the ranks' shard
+renders summed in the reduce's own association (shard.tree_reduce_'s
+pairwise tree), bit for bit.
 """
 from __future__ import annotations
 
@@ -89,14 +90,14 @@ def main(argv=None) -> int:
         ids, part = None, canvas
         spp_mine, seed_base = b.spp, b.seed_base
 
-    def reduce():
+    def reduce():  # the fixed-association tree sum (shard.tree_reduce_)
         if world == 1:
             return
         if a.backend == "nccl":
-            dist.reduce(canvas, dst=0, op=dist.ReduceOp.SUM)
+            shard.tree_reduce_(dist, canvas, torch.empty_like(canvas), rank, world)
         else:
             host = canvas.cpu()
-            dist.reduce(host, dst=0, op=dist.ReduceOp.SUM)
+            shard.tree_reduce_(dist, host, torch.empty_like(host), rank, world)
             if rank == 0:
                 canvas.copy_(host)
 
@@ -158,16 +159,15 @@ def _check(a, dev, cam, canvas, world, stream) -> bool:
         torch.cuda.synchronize()
         want = full[:, :3].cpu().numpy()
         return bool(((got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))).all())
-    acc = np.zeros((n, 3), dtype=np.float32)
     one = torch.empty((n, 4), dtype=torch.float32, device="cuda")
+    parts = []
     for b in shard.sample_batches(a.spp, world, n):
         dev.render_device(cam, a.nx, a.ny, b.spp, a.depth, one.data_ptr(), seed_base=b.seed_base,
                           stream=stream.cuda_stream)
         torch.cuda.synchronize()
-        acc = acc + one[:, :3].cpu().numpy()
-    fin = np.isfinite(acc) & np.isfinite(got)
-    same_nan = np.array_equal(np.isnan(acc), np.isnan(got))
-    return bool(same_nan and np.allclose(got[fin], acc[fin], rtol=1e-6, atol=0))
+        parts.append(one[:, :3].cpu().numpy())
+    want = shard.tree_sum(parts)  # the reduce's own association
+    return bool(((got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))).all())
 
 
 if __name__ == "__main__":

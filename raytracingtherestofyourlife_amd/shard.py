@@ -15,6 +15,12 @@ the framebuffer sum:
   earlier sample's variable draw count, so this is a documented derived
   stream, exact against the oracle run on the same schedule.
 
+The reduce (tree_reduce_) sums in ONE fixed association, the pairwise tree
+((s0 + s1) + (s2 + s3)) + ..., by point-to-point sends.  A collective reduce
+would leave the association of N > 2 float32 shards to the library: RCCL's
+rings follow the node's xGMI topology and split the buffer over channels
+with rings of their own, so the reduced bits would depend on the node.
+
 The render itself is a callback so the planner and the reduce are testable
 on CPU (gloo) with the oracle standing in for the device.
 """
@@ -104,42 +110,86 @@ def render_sample_shard(render: RenderFn, canvas, npix: int, spp: int, rank: int
     return canvas
 
 
+def tree_reduce_(dist, buf, tmp, rank: int, world: int) -> None:
+    """Sum every rank's `buf` into rank 0's `buf` in a fixed association, the
+    pairwise tree ((s0 + s1) + (s2 + s3)) + ... (bench.association_sums
+    "pairwise_tree"; a rank left without a partner passes its partial up
+    unchanged).  Round j (step 2^j): a rank r = 0 mod 2^(j+1) receives rank
+    r + 2^j's partial into `tmp` and adds it (IEEE addition commutes, so only
+    the association is fixed); a rank r = 2^j mod 2^(j+1) sends its partial
+    and is done.  log2(N) rounds of point-to-point transfers, each waiting
+    only on higher ranks: no cycle.  `tmp`: same shape as `buf` (receiving
+    ranks only).  Over RCCL the calls only enqueue: the current stream waits
+    on each transfer on the device."""
+    step = 1
+    while step < world:
+        if rank % (2 * step):
+            dist.send(buf, dst=rank - step)
+            return
+        if rank + step < world:
+            dist.recv(tmp, src=rank + step)
+            buf.add_(tmp)
+        step *= 2
+
+
+def tree_sum(parts):
+    """The float32 sum of the ranks' partials (rank order) in tree_reduce_'s
+    association, on the host: the checker's side of the reduce."""
+    lvl = [np.asarray(p, np.float32) for p in parts]
+    while len(lvl) > 1:
+        lvl = [lvl[i] + lvl[i + 1] if i + 1 < len(lvl) else lvl[i] for i in range(0, len(lvl), 2)]
+    return lvl[0].copy()
+
+
 def reduce_canvas(canvas, dist) -> None:
-    """The one collective: sum the float4 canvases onto rank 0."""
-    if dist.get_world_size() > 1:
-        dist.reduce(canvas, dst=0, op=dist.ReduceOp.SUM)
+    """The framebuffer sum: the ranks' float4 canvases onto rank 0 (tree_reduce_)."""
+    world = dist.get_world_size()
+    if world > 1:
+        tree_reduce_(dist, canvas, canvas.new_empty(canvas.shape), dist.get_rank(), world)
 
 
 class OverlappedCanvasReduce:
     """The per-step canvas reduce of bench.py, overlapped with the next
     step: the rank's entries are scattered into one of two canvases, whose
-    reduce (async) runs while the next step renders; a canvas is reused only
-    after its reduce has been waited on.  overlap=False: one canvas, a
-    synchronous reduce (gloo reduces host tensors: `host_copy` moves a device
-    canvas through the host).  force: run the collective even on one rank
-    (a world-size-1 RCCL group exercises the same calls on a one-GPU box)."""
+    reduce (tree_reduce_) runs on a communication stream while the next step
+    renders; a canvas is reused only after its reduce has finished (an event
+    the render stream waits on, on the device).  Without overlap (host
+    tensors; gloo): one canvas, a synchronous reduce (`host_copy` moves a
+    device canvas through the host).  force: run the reduce's calls even on
+    one rank (a world-size-1 group, where the tree has no transfers)."""
 
     def __init__(self, canvas, dist, overlap: bool, host_copy: bool = False, force: bool = False):
         import torch
 
-        self.dist, self.overlap, self.host_copy = dist, overlap, host_copy
+        self.dist, self.host_copy = dist, host_copy
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.rank = dist.get_rank() if dist.is_initialized() else 0
         self.collective = dist.is_initialized() and (self.world > 1 or force)
-        self.canvases = [canvas, torch.zeros_like(canvas)] if overlap and self.collective else [canvas]
+        # the overlapped path needs device tensors (a stream of its own)
+        self.overlap = overlap and self.collective and canvas.is_cuda and not host_copy
+        self.canvases = [canvas, torch.zeros_like(canvas)] if self.overlap else [canvas]
+        self.tmp = torch.empty_like(canvas) if self.collective and not host_copy else None
+        self.stream = torch.cuda.Stream(device=canvas.device) if self.overlap else None
         self.pending = [None] * len(self.canvases)
         self.steps = 0
+
+    def _wait(self, slot: int) -> None:
+        import torch
+
+        if self.pending[slot] is not None:
+            torch.cuda.current_stream().wait_event(self.pending[slot])
+            self.pending[slot] = None
 
     def step(self, ids, part):
         """Zero the next canvas, scatter `part` at `ids` (ids None: `part` is
         a whole canvas -- a sample batch of every pixel -- and is copied),
         start its reduce; returns that canvas (rank 0 holds the sum once
         drained)."""
+        import torch
+
         slot = self.steps % len(self.canvases)
         self.steps += 1
-        if self.pending[slot] is not None:
-            self.pending[slot].wait()
-            self.pending[slot] = None
+        self._wait(slot)
         c = self.canvases[slot]
         if ids is None:
             c.copy_(part)
@@ -147,22 +197,25 @@ class OverlappedCanvasReduce:
             c.zero_()
             c.index_copy_(0, ids, part)
         if self.collective:
-            if len(self.canvases) > 1:
-                self.pending[slot] = self.dist.reduce(c, dst=0, op=self.dist.ReduceOp.SUM, async_op=True)
+            if self.overlap:
+                self.stream.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(self.stream):
+                    tree_reduce_(self.dist, c, self.tmp, self.rank, self.world)
+                    ev = torch.cuda.Event()
+                    ev.record(self.stream)
+                self.pending[slot] = ev
             elif self.host_copy:
                 host = c.cpu()
-                self.dist.reduce(host, dst=0, op=self.dist.ReduceOp.SUM)
+                tree_reduce_(self.dist, host, torch.empty_like(host), self.rank, self.world)
                 if self.rank == 0:
                     c.copy_(host)
             else:
-                self.dist.reduce(c, dst=0, op=self.dist.ReduceOp.SUM)
+                tree_reduce_(self.dist, c, self.tmp, self.rank, self.world)
         return c
 
     def drain(self) -> None:
-        for i, w in enumerate(self.pending):
-            if w is not None:
-                w.wait()
-                self.pending[i] = None
+        for i in range(len(self.pending)):
+            self._wait(i)
 
 
 def sample_shard_consistency(single: np.ndarray, shards: list, spp: int) -> dict:

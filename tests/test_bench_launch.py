@@ -72,11 +72,18 @@ def test_reduced_frame_parity(n):
     f = bench.find_reduced_fixture(3840, 2160, 16384, 50, n)
     shards = [np.c_[s, np.zeros(len(s), np.float32)] for s in f["shards"]]
     sums = bench.association_sums(f["shards"])
+    tree = sums["pairwise_tree" if n > 2 else "rank_order"]  # the reduce's own association (shard.tree_reduce_)
     for name, red in sums.items():
         p = bench.reduced_frame_parity(f, shards, red, 16384)
-        assert p["bit_exact"] and p["shards_bit_exact"], (name, p)
+        assert p["shards_bit_exact"], (name, p)
         assert p["reduced_association"][name] == 1024 and p["reduced_pixels_matching_an_association"] == 1024
+        # bit_exact: the reduce's association only (another one passes where it happens to agree)
+        same = bool(bench._same_bits(red, tree).all())
+        assert p["bit_exact"] == same and p["reduced_bit_exact_tree"] == same, (name, p)
         assert p["rmse"] < (1e-6 if n > 2 else 1e-30)
+    assert bench.reduced_frame_parity(f, shards, tree, 16384)["bit_exact"]
+    if n == 8:  # RCCL-style rank-order chains are not the reduce's bits
+        assert not bench.reduced_frame_parity(f, shards, sums["rank_order"], 16384)["bit_exact"]
     assert bench.reduced_frame_parity(f, shards, f["reduced"], 16384)["rmse"] == 0.0
     # one ulp off in one shard's pixel: the shard check and the line's bit_exact fail
     bad = [s.copy() for s in shards]

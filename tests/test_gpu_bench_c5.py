@@ -5,8 +5,8 @@ canvas.  Rank k renders spp/N samples of every pixel on its derived stream
 (seed_base k*nx*ny).  The line's parity comes from the oracle's reduced-frame
 fixture of that N (tests/golden/c5_reduced_small.npz,
 tools/make_golden_reduced.py): every rank's shard bit-exact, the reduced frame
-bit-exact (two ranks: one float add; more: the sum in the reduce's
-association) and rmse 0 at N = 2.  Rank 0 then renders the whole frame alone
+bit-exact (two ranks: one float add; more: the sum in the reduce's fixed
+association, shard.tree_reduce_'s pairwise tree) and rmse 0 at N = 2.  Rank 0 then renders the whole frame alone
 on an unused stream (the same-workload one-GPU anchor) and checks the reduced
 canvas statistically against it (shard.sample_shard_ttest)."""
 from __future__ import annotations
@@ -57,4 +57,7 @@ def test_bench_c5_four_ranks_reduced_parity():
     par = line["reduced_frame_parity"]
     assert par["ranks"] == 4 and par["shards_bit_exact"], par
     assert par["bit_exact"] is True and line["bit_exact"] is True, json.dumps(par)
+    assert par["reduced_bit_exact_tree"] is True  # ((s0 + s1) + (s2 + s3)), every pixel
     assert line["rmse"] < 1e-6
+    chk = line["check_reduced_canvas"]
+    assert chk["reduced_equals_sum_of_shards_max_rel"] == 0.0 and chk["nan_pattern_equal"]

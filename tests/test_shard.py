@@ -215,3 +215,57 @@ def test_overlapped_reduce_of_sample_batches(tmp_path, overlap):
     want = parts[0] + parts[1]
     assert np.isnan(want[:, :3]).any()
     assert _same(got[:, :3], want[:, :3])
+
+
+def _tree_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from raytracingtherestofyourlife_amd import shard
+
+    buf = torch.from_numpy(_tree_parts(world)[rank].copy())
+    shard.tree_reduce_(dist, buf, torch.empty_like(buf), rank, world)
+    if rank == 0:
+        np.save(out_path, buf.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _tree_parts(world):
+    # magnitudes spread over many binades: float32 sums of more than two of
+    # them depend on the association
+    rng = np.random.default_rng(11)
+    return [(rng.standard_normal((256, 4)) * 10.0 ** rng.integers(-3, 4, (256, 4))).astype(np.float32)
+            for _ in range(world)]
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 5])
+def test_tree_reduce_fixed_association(tmp_path, world):
+    """shard.tree_reduce_ (bench.py's and render_dist's framebuffer sum) over
+    gloo: rank 0 ends with the pairwise-tree sum ((s0 + s1) + (s2 + s3)) + ...
+    bit for bit (shard.tree_sum, the checker's side), whatever the world size,
+    including a rank left without a partner."""
+    from raytracingtherestofyourlife_amd import shard
+
+    out = str(tmp_path / "tree.npy")
+    mp.start_processes(_tree_worker, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
+    got = np.load(out)
+    parts = _tree_parts(world)
+    want = shard.tree_sum(parts)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    if world >= 4:  # (three ranks: (s0 + s1) + s2 IS rank order) the test data tells the associations apart
+        chain = parts[0].copy()
+        for p in parts[1:]:
+            chain = chain + p
+        assert not np.array_equal(chain.view(np.uint32), want.view(np.uint32))
+
+
+def test_tree_sum_matches_bench_pairwise_tree():
+    import bench
+    from raytracingtherestofyourlife_amd import shard
+
+    for world in (3, 4, 6, 8):
+        parts = _tree_parts(world)
+        assert np.array_equal(bench.association_sums(parts)["pairwise_tree"], shard.tree_sum(parts))
+    s = _tree_parts(6)
+    want = ((s[0] + s[1]) + (s[2] + s[3])) + (s[4] + s[5])
+    assert np.array_equal(shard.tree_sum(s).view(np.uint32), want.view(np.uint32))
