@@ -217,29 +217,35 @@ def test_c5_rank_share_whole_canvas_digest(device, tables_on, name):
     assert canonical_rgb_sha256(rgb) == bytes(g["rgb_sha256"]), "rgb sums differ"
 
 
-@pytest.mark.skipif(not os.path.exists(os.path.join(GOLD, "c3_full16_digest.npz")),
-                    reason="tests/golden/c3_full16_digest.npz not generated (tools/make_golden_digest.py)")
-def test_c3_whole_canvas_digest(device, tables_on):
-    """C3's whole canvas (2048^2, 1000 spheres, depth 50) at 16 spp (the
-    oracle's full-spp frame would take ~8 h on the host; c3_subset4k covers
-    4096 pixels at the full 256) against the oracle's digests: every one of
-    the 4.2 M pixels through the sphere-BVH walk on the work-stealing
-    schedule -- rgb sums (NaN canonical), NaN pixels, final seeds, live counts."""
+C3_DIGESTS = [n for n in ("c3_full16_digest", "c3_band256_digest") if os.path.exists(os.path.join(GOLD, n + ".npz"))]
+
+
+@pytest.mark.skipif(not C3_DIGESTS, reason="no C3 digest generated (tools/make_golden_digest.py)")
+@pytest.mark.parametrize("name", C3_DIGESTS)
+def test_c3_whole_canvas_digest(device, tables_on, name):
+    """C3 (2048^2, 1000 spheres, depth 50) against the oracle's digests over
+    the fixture's pixels: c3_full16_digest, the whole canvas at 16 spp (the
+    oracle's full-spp frame would take ~8 h on the host); c3_band256_digest,
+    a leading band of rows at the full 256 spp (`pixel_count`,
+    tools/make_golden_digest.py --assemble-first); c3_subset4k covers 4096
+    scattered pixels at 256.  Every pixel goes through the sphere-BVH walk on
+    the work-stealing schedule: rgb sums (NaN canonical), NaN pixels, final
+    seeds, live counts."""
     import torch
 
     import raytracingtherestofyourlife_amd as rtp
 
     from _util import canonical_rgb_sha256, sha256_u32
 
-    g = _load("c3_full16_digest")
+    g = _load(name)
     device.set_cornell_box(int(g["variant"]))
     nx, ny, spp, depth = int(g["nx"]), int(g["ny"]), int(g["spp"]), int(g["depth"])
-    n = nx * ny
-    assert int(g["pixel_count"]) == n and int(g["seed_base"]) == 0
+    n = int(g["pixel_count"])
+    assert int(g.get("pixel_begin", 0)) == 0 and int(g["seed_base"]) == 0 and 0 < n <= nx * ny
     out = torch.empty((n, 4), dtype=torch.float32, device="cuda")
     seeds = torch.empty(n, dtype=torch.int32, device="cuda")
     live = torch.empty(n, dtype=torch.int32, device="cuda")
-    device.render_device(rtp.default_camera(), nx, ny, spp, depth, out.data_ptr(),
+    device.render_device(rtp.default_camera(), nx, ny, spp, depth, out.data_ptr(), pixel_count=n,
                          stream=torch.cuda.current_stream().cuda_stream, seed_ptr=seeds.data_ptr(),
                          live_ptr=live.data_ptr())
     torch.cuda.synchronize()
