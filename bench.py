@@ -147,6 +147,8 @@ def load_golden_frame(path: str, any_seed: bool = False):
         z = np.load(path, allow_pickle=False)
     except OSError:
         return None
+    if "rgb_planes" not in z.files and "rgb" not in z.files:
+        return None  # not a frame fixture (c5_reduced.npz: the N > 1 shards, reduced_frame_parity)
     if "rgb_planes" in z.files:
         rgb, pixels = np.ascontiguousarray(z["rgb_planes"].T).view(np.float32).reshape(-1, 3), None
     else:
